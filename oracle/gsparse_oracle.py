@@ -1,0 +1,325 @@
+"""CPU oracle for the edge-scoring hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module, and only as the checker (or as
+the timed CPU baseline).  The product (``gsparse``) never imports it and
+fails loudly when its HIP library is missing.
+
+It restates the reference path ``/root/reference/src/sparsification`` in
+NumPy/SciPy plus a small C library (``oracle.c``, built by ``make -C
+oracle``), each function citing the reference file:line it follows.  Parity
+is PINNED: ``tests/test_oracle_golden.py`` checks every function here against
+golden vectors produced by running the reference itself in the build
+container (``tests/golden/make_golden.py``).  ApproxER is pinned within the
+reference's own BLAS-order envelope: its CG dot
+products go to OpenBLAS ``ddot``, whose reduction order is not reproducible.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import scipy.sparse as sp
+import scipy.sparse.linalg as spla
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_f64p = ctypes.POINTER(ctypes.c_double)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "_build", "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.oracle_pairwise_sum_f64.restype = ctypes.c_double
+        L.oracle_pairwise_sum_f32.restype = ctypes.c_float
+        L.oracle_metric_backbone.restype = ctypes.c_int64
+        L.oracle_ddot.restype = ctypes.c_double
+        _LIB = L
+    return _LIB
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+# ----------------------------------------------------------------------------
+# graph construction
+def canonical_csr(edge_index: np.ndarray, n: int):
+    """core.py:70-74: sp.csr_matrix((ones(E), (ei0, ei1)), (n, n)).
+
+    Canonical CSR: duplicates summed (data = multiplicity), columns sorted.
+    Returns (indptr int64, indices int32, data float64)."""
+    ei = np.asarray(edge_index, dtype=np.int64)
+    keys = ei[0] * np.int64(n) + ei[1]
+    uniq, counts = np.unique(keys, return_counts=True)
+    rows = uniq // n
+    indices = (uniq % n).astype(np.int32)
+    indptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(rows, minlength=n), out=indptr[1:])
+    return indptr, indices, counts.astype(np.float64)
+
+
+def transpose(indptr, indices, n):
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(indptr))
+    order = np.lexsort((rows, indices.astype(np.int64)))
+    tix = rows[order].astype(np.int32)
+    tp = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(indices, minlength=n), out=tp[1:])
+    return tp, tix
+
+
+def csr_rows(indptr):
+    n = len(indptr) - 1
+    return np.repeat(np.arange(n, dtype=np.int64), np.diff(indptr))
+
+
+# ----------------------------------------------------------------------------
+# scorers (metrics.py)
+def jaccard(indptr, indices):
+    """metrics.py:17-64 (integer counts, one fp64 divide)."""
+    n = len(indptr) - 1
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(indices, dtype=np.int32)
+    tp, ti = transpose(indptr, indices, n)
+    out = np.zeros(len(indices), dtype=np.float64)
+    lib().oracle_jaccard(ctypes.c_int64(n), _p(indptr, _i64p), _p(indices, _i32p),
+                         _p(tp, _i64p), _p(ti, _i32p), _p(out, _f64p))
+    return out
+
+
+def aa_weights(indptr):
+    """metrics.py:100-108: c = 1/sqrt(max(log(deg+1), 1e-10)) with NumPy ufuncs."""
+    deg = np.diff(indptr).astype(np.float64)
+    log_degrees = np.maximum(np.log(deg + 1), 1e-10)
+    return 1.0 / np.sqrt(log_degrees)
+
+
+def adamic_adar(indptr, indices):
+    """metrics.py:67-121 (descending-id fold of c_w*c_w from 0.0)."""
+    n = len(indptr) - 1
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(indices, dtype=np.int32)
+    c = np.ascontiguousarray(aa_weights(indptr))
+    out = np.zeros(len(indices), dtype=np.float64)
+    lib().oracle_adamic_adar(ctypes.c_int64(n), _p(indptr, _i64p), _p(indices, _i32p),
+                             _p(c, _f64p), _p(out, _f64p))
+    return out
+
+
+def degree(indptr, indices, data):
+    """core.py:167-172: deg = adj.sum(1) (multiplicity-weighted); deg[r]*deg[c]."""
+    n = len(indptr) - 1
+    rows = csr_rows(indptr)
+    deg = np.bincount(rows, weights=data, minlength=n)
+    return deg[rows] * deg[indices]
+
+
+def feature_cosine(indptr, indices, x):
+    """metrics.py:301-358, restated with an explicit NumPy-pairwise C loop."""
+    n = len(indptr) - 1
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(indices, dtype=np.int32)
+    out = np.zeros(len(indices), dtype=np.float64)
+    f = x.shape[1]
+    if x.dtype == np.float32:
+        xx = np.ascontiguousarray(x)
+        lib().oracle_feature_cosine_f32(ctypes.c_int64(n), ctypes.c_int64(f), _p(indptr, _i64p),
+                                        _p(indices, _i32p), _p(xx, _f32p), _p(out, _f64p))
+    else:
+        xx = np.ascontiguousarray(x, dtype=np.float64)
+        lib().oracle_feature_cosine_f64(ctypes.c_int64(n), ctypes.c_int64(f), _p(indptr, _i64p),
+                                        _p(indices, _i32p), _p(xx, _f64p), _p(out, _f64p))
+    return out
+
+
+def jl_dim(n: int, epsilon: float = 0.3) -> int:
+    """metrics.py:248."""
+    return max(int(24 * np.log(max(n, 2)) / (epsilon ** 2)), 1)
+
+
+def laplacian_reg(indptr, indices, data, n, reg=1e-6):
+    """metrics.py:251-256: L = diag(rowsum A) - A; L_reg = L + 1e-6 I (SciPy canonical)."""
+    adj = sp.csr_matrix((data, indices, indptr), shape=(n, n))
+    degrees = np.array(adj.sum(axis=1)).flatten()
+    L = sp.diags(degrees, format="csr") - adj
+    L_reg = L + reg * sp.eye(n, format="csr")
+    L_reg.sort_indices()
+    return L_reg
+
+
+def approx_er_projection(indptr, indices, n, epsilon=0.3, seed=42):
+    """metrics.py:232-275: edges u<v in CSR order, k, R = N(0,1)^{m x k}/sqrt(k), Y = B @ R."""
+    rows = csr_rows(indptr)
+    mask = rows < indices
+    u_e, v_e = rows[mask], indices[mask].astype(np.int64)
+    m = len(u_e)
+    k = jl_dim(n, epsilon)
+    rng = np.random.default_rng(seed)
+    B = sp.csr_matrix((np.concatenate([np.ones(m), -np.ones(m)]),
+                       (np.concatenate([u_e, v_e]), np.concatenate([np.arange(m), np.arange(m)]))),
+                      shape=(n, m))
+    R = rng.standard_normal((m, k)) / np.sqrt(k)
+    return B @ R, m, k
+
+
+def approx_er(indptr, indices, data, n, epsilon=0.3, seed=42, max_cg_iters=500, cg_tol=1e-6,
+              impl="scipy", blas_threads=1, return_z=False):
+    """metrics.py:178-298.
+
+    impl="scipy": SciPy cg exactly as the reference calls it (this host's
+    OpenBLAS decides the ddot order).  impl="c": the restated CG of oracle.c
+    with the OpenBLAS-SkylakeX ddot order for ``blas_threads`` threads.
+    """
+    rows = csr_rows(indptr)
+    if np.count_nonzero(rows < indices) == 0:
+        return np.zeros(len(indices), dtype=np.float64)
+    Y, m, k = approx_er_projection(indptr, indices, n, epsilon, seed)
+    L_reg = laplacian_reg(indptr, indices, data, n)
+    if impl == "scipy":
+        import warnings
+        Z = np.zeros((n, k), dtype=np.float64)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", RuntimeWarning)
+            for i in range(k):
+                z, info = spla.cg(L_reg, Y[:, i], maxiter=max_cg_iters, rtol=cg_tol)
+                if info != 0 or np.any(np.isnan(z)):
+                    z = np.nan_to_num(z, nan=0.0, posinf=0.0, neginf=0.0)
+                Z[:, i] = z
+        diff = Z[rows] - Z[indices]
+        r_eff = np.sum(diff ** 2, axis=1)
+        r_eff = np.nan_to_num(r_eff, nan=1e-10, posinf=1e-10, neginf=1e-10)
+        out = np.maximum(r_eff, 1e-10)
+    else:
+        Z, _ = cg(L_reg, Y, max_cg_iters, cg_tol, blas_threads)
+        out = er_from_z(indptr, indices, Z)
+    return (out, Z) if return_z else out
+
+
+def cg(L_reg, Y, maxiter=500, rtol=1e-6, blas_threads=1):
+    n, k = Y.shape
+    lp = np.ascontiguousarray(L_reg.indptr, dtype=np.int64)
+    li = np.ascontiguousarray(L_reg.indices, dtype=np.int32)
+    lv = np.ascontiguousarray(L_reg.data, dtype=np.float64)
+    Yc = np.ascontiguousarray(Y, dtype=np.float64)
+    Z = np.zeros((n, k), dtype=np.float64)
+    its = np.zeros(k, dtype=np.int32)
+    lib().oracle_cg(ctypes.c_int64(n), _p(lp, _i64p), _p(li, _i32p), _p(lv, _f64p),
+                    ctypes.c_int64(k), _p(Yc, _f64p), ctypes.c_int32(maxiter),
+                    ctypes.c_double(rtol), ctypes.c_int32(blas_threads), _p(Z, _f64p),
+                    _p(its, _i32p))
+
+    return Z, its
+
+
+def er_from_z(indptr, indices, Z):
+    n, k = Z.shape
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(indices, dtype=np.int32)
+    Zc = np.ascontiguousarray(Z)
+    out = np.zeros(len(indices), dtype=np.float64)
+    lib().oracle_er_from_z(ctypes.c_int64(n), _p(indptr, _i64p), _p(indices, _i32p),
+                           ctypes.c_int64(k), _p(Zc, _f64p), _p(out, _f64p))
+    return out
+
+
+# ----------------------------------------------------------------------------
+# selection (core.py)
+def topk_mask(scores, num_edges, retention_ratio, keep_lowest=False, kind=None):
+    """core.py:221-242.  kind=None: np.argsort default (the reference's
+    unstable sort); kind='stable': the tie rule the HIP top-k implements."""
+    if not 0 < retention_ratio <= 1:
+        raise ValueError(f"retention_ratio must be in (0, 1], got {retention_ratio}")
+    if retention_ratio == 1.0:
+        return np.ones(num_edges, dtype=bool)
+    num_keep = int(num_edges * retention_ratio)
+    idx = np.argsort(scores) if kind is None else np.argsort(scores, kind=kind)
+    sel = idx[:num_keep] if keep_lowest else idx[-num_keep:]
+    mask = np.zeros(num_edges, dtype=bool)
+    mask[sel] = True
+    return mask
+
+
+def scores_to_cost(scores, metric_key):
+    """core.py:82-116 (metric_key already normalised)."""
+    if metric_key in ("effective_resistance", "approx_effective_resistance"):
+        similarity = 1.0 / np.maximum(scores, 1e-10)
+    else:
+        similarity = scores.copy()
+    s_max = similarity.max()
+    if s_max <= 0:
+        return np.ones_like(scores)
+    proximity = similarity / s_max
+    nonzero = proximity[proximity > 0]
+    floor = (nonzero.min() * 0.01) if len(nonzero) > 0 else 1e-6
+    proximity[proximity <= 0] = floor
+    return 1.0 / proximity - 1.0
+
+
+def metric_backbone(edge_index, n, w, epsilon=1e-9, return_relax=False):
+    """metric_backbone.py:59-111 restated as bounded per-row Dijkstra (oracle.c)."""
+    ei = np.asarray(edge_index, dtype=np.int64)
+    rows, cols = np.ascontiguousarray(ei[0]), np.ascontiguousarray(ei[1])
+    E = len(rows)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    if len(w) < E:
+        raise IndexError(f"index {len(w)} is out of bounds for axis 0 with size {len(w)}")
+    # G: u<v columns, min weight over duplicates (metric_backbone.py:70-79)
+    m = rows < cols
+    gu, gv, gw = rows[m], cols[m], w[:E][m]
+    keys = gu * n + gv
+    order = np.lexsort((gw, keys))
+    keys, gw = keys[order], gw[order]
+    first = np.ones(len(keys), dtype=bool)
+    first[1:] = keys[1:] != keys[:-1]
+    keys, gw = keys[first], gw[first]
+    gu, gv = keys // n, keys % n
+    src = np.concatenate([gu, gv])
+    dst = np.concatenate([gv, gu])
+    ww = np.concatenate([gw, gw])
+    o = np.lexsort((dst, src))
+    src, dst, ww = src[o], dst[o], ww[o]
+    gp = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(src, minlength=n), out=gp[1:])
+    gi = np.ascontiguousarray(dst, dtype=np.int32)
+    gw_ = np.ascontiguousarray(ww)
+    corder = np.argsort(rows, kind="stable").astype(np.int64)
+    optr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(rows, minlength=n), out=optr[1:])
+    keep = np.zeros(E, dtype=np.uint8)
+    relax = ctypes.c_int64(0)
+    lib().oracle_metric_backbone(ctypes.c_int64(n), _p(gp, _i64p), _p(gi, _i32p), _p(gw_, _f64p),
+                                 ctypes.c_int64(E), _p(rows, _i64p), _p(cols, _i64p), _p(w, _f64p),
+                                 ctypes.c_double(epsilon), _p(corder, _i64p), _p(optr, _i64p),
+                                 _p(keep, _u8p), ctypes.byref(relax))
+    keep = keep.astype(bool)
+    return (keep, relax.value) if return_relax else keep
+
+
+def sampled_mask(scores, num_edges, retention_ratio, seed=42):
+    """core.py:333-350."""
+    rng = np.random.default_rng(seed)
+    floor = 1e-8
+    s = np.nan_to_num(scores, nan=floor, posinf=floor, neginf=floor)
+    probs = np.maximum(s, floor)
+    probs = probs / probs.sum()
+    num_keep = int(num_edges * retention_ratio)
+    selected = rng.choice(num_edges, size=num_keep, replace=False, p=probs)
+    mask = np.zeros(num_edges, dtype=bool)
+    mask[selected] = True
+    return mask
