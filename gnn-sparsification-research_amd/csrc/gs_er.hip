@@ -1,0 +1,770 @@
+// gs_er.hip -- ApproxER (calculate_approx_effective_resistance_scores,
+// metrics.py:178-298) on the device, bit-exact with the reference.
+//
+// Layout in HBM (row-major n x k, the JL columns contiguous per node):
+//   Rr  residual, initialised with Y = B @ R           (metrics.py:275)
+//   X   solution, P0/P1 search direction (ping-pong), Q = L_reg p
+// The k CG solves (metrics.py:284-289, SciPy 1.15 cg recurrence) run as one
+// batched iteration: per iteration two fused streaming kernels
+//   k_cg_pq : p = beta*p + r (two roundings) ; q = L_reg p (per-row fold from
+//             0.0 in ascending column, products rounded) ; partial dot(p,q)
+//   k_cg_upd: x += fl(alpha p) ; r -= fl(alpha q) ; partial dot(r,r)
+// plus two per-column finish kernels.  Every dot product reproduces
+// OpenBLAS ddot (SkylakeX kernel) as np.dot calls it: T thread chunks for
+// n > 10000, inside a chunk 32 FMA accumulator chains over rows j, j+32, ...,
+// then the 32->16 fold, the optional 16-block, the 4-lane tree and the FMA
+// tail (pinned in oracle.c, oracle_ddot).  A lane of k_cg_* owns one
+// (column, chunk, residue j) chain: the chain IS the thread's row loop, so
+// the reduction costs no extra pass over HBM.
+#include "gs_internal.hpp"
+#include "gs_pairwise.hpp"
+
+namespace gs {
+
+static constexpr int kMaxChunks = 64;
+
+struct Chunks {
+    int32_t count;
+    int64_t a[kMaxChunks];
+    int64_t len[kMaxChunks];
+};
+
+static Chunks make_chunks(int64_t n, int32_t threads) {
+    Chunks ch{};
+    if (n <= 10000 || threads <= 1) {
+        ch.count = 1;
+        ch.a[0] = 0;
+        ch.len[0] = n;
+        return ch;
+    }
+    if (threads > kMaxChunks) threads = kMaxChunks;
+    int64_t lo = 0, rem = n;
+    int32_t cnt = 0;
+    for (int32_t t = threads; t > 0 && rem > 0; --t) {
+        int64_t w = (rem + t - 1) / t;
+        ch.a[cnt] = lo;
+        ch.len[cnt] = w;
+        ++cnt;
+        lo += w;
+        rem -= w;
+    }
+    ch.count = cnt;
+    return ch;
+}
+
+// per-column state, structure of arrays inside one buffer
+struct ColPtrs {
+    double *bn, *atol, *rho, *rho_prev, *alpha;
+    int32_t *active, *iters;
+    int32_t *nactive;  // single counter
+};
+
+static ColPtrs col_ptrs(ErState &er) {
+    int64_t k = er.k;
+    char *b = (char *)er.colstate.ptr;
+    ColPtrs p;
+    p.bn = (double *)b;
+    p.atol = p.bn + k;
+    p.rho = p.atol + k;
+    p.rho_prev = p.rho + k;
+    p.alpha = p.rho_prev + k;
+    p.active = (int32_t *)(p.alpha + k);
+    p.iters = p.active + k;
+    p.nactive = p.iters + k;
+    return p;
+}
+
+// ---------------------------------------------------------------- prepare
+__global__ void k_upper_flags(const int32_t *__restrict__ rows, const int32_t *__restrict__ ix,
+                              int64_t nnz, int64_t *__restrict__ flag) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz;
+         e += (int64_t)gridDim.x * blockDim.x)
+        flag[e] = rows[e] < ix[e] ? 1 : 0;
+}
+
+__global__ void k_edge_ids(const int64_t *__restrict__ flag, const int64_t *__restrict__ pos,
+                           int64_t nnz, int64_t *__restrict__ eid) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz;
+         e += (int64_t)gridDim.x * blockDim.x)
+        eid[e] = flag[e] ? pos[e] : -1;
+}
+
+// B row counts: node i is incident to (u,i) u<i (transposed column i) and (i,j) j>i (row i).
+__global__ void k_b_counts(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                           const int64_t *__restrict__ tp, const int32_t *__restrict__ ti,
+                           int64_t n, int64_t *__restrict__ cnt) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t c = 0;
+        for (int64_t t = tp[i]; t < tp[i + 1]; ++t) c += ti[t] < i;
+        for (int64_t e = ip[i]; e < ip[i + 1]; ++e) c += ix[e] > i;
+        cnt[i] = c;
+    }
+}
+
+__global__ void k_b_fill(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                         const int64_t *__restrict__ tp, const int32_t *__restrict__ ti,
+                         const int64_t *__restrict__ tpos, const int64_t *__restrict__ eid,
+                         int64_t n, const int64_t *__restrict__ bptr, int64_t *__restrict__ bcol,
+                         int8_t *__restrict__ bsgn, int64_t *__restrict__ bcur) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t o = bptr[i];
+        bcur[i] = o;
+        // (u, i) with u < i: edge ids ascending with u (row-major numbering), sign -1
+        for (int64_t t = tp[i]; t < tp[i + 1]; ++t)
+            if (ti[t] < i) {
+                bcol[o] = eid[tpos[t]];
+                bsgn[o] = -1;
+                ++o;
+            }
+        // (i, j) with j > i: after every (u, i), sign +1
+        for (int64_t e = ip[i]; e < ip[i + 1]; ++e)
+            if (ix[e] > i) {
+                bcol[o] = eid[e];
+                bsgn[o] = 1;
+                ++o;
+            }
+    }
+}
+
+// L = diag(rowsum A) - A (zeros dropped, SciPy csr_minus), L_reg = L + reg I.
+__device__ __forceinline__ void lrow_diag(const int64_t *ip, const int32_t *ix, const double *d,
+                                          int64_t i, double reg, double &diag, bool &has_diag) {
+    double deg = 0.0, aii = 0.0;
+    bool self = false;
+    for (int64_t e = ip[i]; e < ip[i + 1]; ++e) {
+        deg = deg + d[e];  // adj.sum(axis=1): fold ascending column from 0.0
+        if (ix[e] == i) {
+            self = true;
+            aii = d[e];
+        }
+    }
+    // D_ii present iff deg != 0 (dia->csr drops zeros)
+    bool has_l = false;
+    double l = 0.0;
+    if (deg != 0.0 && self) {
+        l = deg - aii;
+        has_l = l != 0.0;
+    } else if (deg != 0.0) {
+        l = deg;
+        has_l = true;
+    } else if (self) {
+        l = 0.0 - aii;
+        has_l = l != 0.0;
+    }
+    diag = has_l ? l + reg : reg;
+    has_diag = diag != 0.0;
+}
+
+__global__ void k_l_counts(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                           const double *__restrict__ d, int64_t n, double reg,
+                           int64_t *__restrict__ cnt) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double dg;
+        bool hd;
+        lrow_diag(ip, ix, d, i, reg, dg, hd);
+        int64_t c = hd ? 1 : 0;
+        for (int64_t e = ip[i]; e < ip[i + 1]; ++e)
+            if (ix[e] != i && d[e] != 0.0) ++c;
+        cnt[i] = c;
+    }
+}
+
+__global__ void k_l_fill(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                         const double *__restrict__ d, int64_t n, double reg,
+                         const int64_t *__restrict__ lp, int32_t *__restrict__ li,
+                         double *__restrict__ lv) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double dg;
+        bool hd;
+        lrow_diag(ip, ix, d, i, reg, dg, hd);
+        int64_t o = lp[i];
+        bool placed = !hd;
+        for (int64_t e = ip[i]; e < ip[i + 1]; ++e) {
+            int32_t j = ix[e];
+            if (!placed && j >= i) {
+                li[o] = (int32_t)i;
+                lv[o] = dg;
+                ++o;
+                placed = true;
+            }
+            if (j != i && d[e] != 0.0) {
+                li[o] = j;
+                lv[o] = 0.0 - d[e];
+                ++o;
+            }
+        }
+        if (!placed) {
+            li[o] = (int32_t)i;
+            lv[o] = dg;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- projection
+// Y[i,:] += sign * raw[e - e0, :] / sqrt_k for node i's incident edges e in
+// [e0, e1), in ascending e (metrics.py:272-275; SciPy csr_matvecs folds B's
+// sorted row from 0.0, +-1 * R exact).  One block (64 lanes) per node and
+// 64-column slice.
+__global__ void __launch_bounds__(256) k_project(const int64_t *__restrict__ bptr,
+                                                 const int64_t *__restrict__ bcol,
+                                                 const int8_t *__restrict__ bsgn,
+                                                 int64_t *__restrict__ bcur, int64_t n, int64_t k,
+                                                 int64_t e0, int64_t e1,
+                                                 const double *__restrict__ raw, double sqrt_k,
+                                                 double *__restrict__ Y) {
+    int64_t ncb = (k + 63) / 64;
+    int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    int lane = threadIdx.x & 63;
+    int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t w = wave; w < n * ncb; w += nwaves) {
+        int64_t i = w / ncb, cb = w % ncb;
+        int64_t c = cb * 64 + lane;
+        int64_t cur = bcur[i], end = bptr[i + 1];
+        int64_t p = cur;
+        double y = (c < k) ? Y[i * k + c] : 0.0;
+        for (; p < end; ++p) {
+            int64_t e = bcol[p];
+            if (e >= e1) break;
+            if (c < k) {
+                double r = raw[(e - e0) * k + c] / sqrt_k;
+                double t = bsgn[p] > 0 ? r : -r;
+                y = y + t;
+            }
+        }
+        if (c < k) Y[i * k + c] = y;
+        if (cb == ncb - 1 && lane == 0) bcur[i] = p;  // last slice advances the cursor
+    }
+}
+
+// ---------------------------------------------------------------- CG kernels
+struct ChunkArg {
+    int32_t count;
+    int64_t a[kMaxChunks];
+    int64_t len[kMaxChunks];
+};
+
+// Grid: x = column blocks of 64, y = residue groups (4 per block -> 8 groups
+// cover j = 0..31), z = chunk.  Block = 256 threads = 4 waves; wave w holds
+// residue j = 4*blockIdx.y + w for 64 consecutive columns (512-B coalesced rows).
+struct CgGeom {
+    int64_t n, k, col0, col1;
+};
+
+__device__ __forceinline__ int64_t wave_uniform(int64_t v) {
+    return ((int64_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(v & 0xffffffff));
+}
+
+template <bool FIRST>
+__global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
+                                               const int64_t *__restrict__ lp,
+                                               const int32_t *__restrict__ li,
+                                               const double *__restrict__ lv,
+                                               const double *__restrict__ R,
+                                               const double *__restrict__ Pold,
+                                               double *__restrict__ Pnew, double *__restrict__ Q,
+                                               const double *__restrict__ rho,
+                                               const double *__restrict__ rho_prev,
+                                               const int32_t *__restrict__ active,
+                                               double *__restrict__ acc) {
+    const int64_t k = G.k;
+    const int64_t c = G.col0 + blockIdx.x * 64 + (threadIdx.x & 63);
+    const int j = __builtin_amdgcn_readfirstlane((int)(blockIdx.y * 4 + (threadIdx.x >> 6)));
+    const int t = blockIdx.z;
+    const bool live = c < G.col1 && active[c];
+    double beta = 0.0;
+    if (!FIRST && live) beta = rho[c] / rho_prev[c];
+    const int64_t a = ch.a[t], L = ch.len[t];
+    const int64_t n1 = L & ~(int64_t)15, n32 = n1 & ~(int64_t)31;
+    double s = 0.0;
+    auto pnew = [&](int64_t row) -> double {
+        double r = R[row * k + c];
+        if (FIRST) return r;
+        double pb = Pold[row * k + c] * beta;
+        return pb + r;
+    };
+    if (!live) return;
+    // main region: rows a + j + 32 s, FMA chain
+    for (int64_t row = a + j; row < a + n32; row += 32) {
+        int64_t e0 = lp[row], e1 = lp[row + 1];
+        double q = 0.0, pi = 0.0;
+        bool found = false;
+        for (int64_t e = e0; e < e1; ++e) {
+            int32_t col = li[e];
+            double pv = pnew(col);
+            if (col == row) {
+                pi = pv;
+                found = true;
+            }
+            double prod = lv[e] * pv;
+            q = q + prod;
+        }
+        if (!found) pi = pnew(row);
+        Pnew[row * k + c] = pi;
+        Q[row * k + c] = q;
+        s = __builtin_fma(pi, q, s);
+    }
+    // leftover rows of the chunk (16-block + tail): computed, not accumulated
+    {
+        int64_t row = a + n32 + j;
+        if (row < a + L) {
+            int64_t e0 = lp[row], e1 = lp[row + 1];
+            double q = 0.0, pi = 0.0;
+            bool found = false;
+            for (int64_t e = e0; e < e1; ++e) {
+                int32_t col = li[e];
+                double pv = pnew(col);
+                if (col == row) {
+                    pi = pv;
+                    found = true;
+                }
+                double prod = lv[e] * pv;
+                q = q + prod;
+            }
+            if (!found) pi = pnew(row);
+            Pnew[row * k + c] = pi;
+            Q[row * k + c] = q;
+        }
+    }
+    acc[((c - G.col0) * kMaxChunks + t) * 32 + j] = s;
+}
+
+__global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
+                                                const double *__restrict__ P,
+                                                const double *__restrict__ Q,
+                                                double *__restrict__ X, double *__restrict__ R,
+                                                const double *__restrict__ alpha,
+                                                const int32_t *__restrict__ active,
+                                                double *__restrict__ acc) {
+    const int64_t k = G.k;
+    const int64_t c = G.col0 + blockIdx.x * 64 + (threadIdx.x & 63);
+    const int j = __builtin_amdgcn_readfirstlane((int)(blockIdx.y * 4 + (threadIdx.x >> 6)));
+    const int t = blockIdx.z;
+    if (!(c < G.col1 && active[c])) return;
+    const double al = alpha[c];
+    const int64_t a = ch.a[t], L = ch.len[t];
+    const int64_t n1 = L & ~(int64_t)15, n32 = n1 & ~(int64_t)31;
+    double s = 0.0;
+    for (int64_t row = a + j; row < a + n32; row += 32) {
+        int64_t o = row * k + c;
+        double t1 = al * P[o];
+        double x = X[o] + t1;
+        double t2 = al * Q[o];
+        double r = R[o] - t2;
+        X[o] = x;
+        R[o] = r;
+        s = __builtin_fma(r, r, s);
+    }
+    int64_t row = a + n32 + j;
+    if (row < a + L) {
+        int64_t o = row * k + c;
+        double t1 = al * P[o];
+        double t2 = al * Q[o];
+        X[o] = X[o] + t1;
+        R[o] = R[o] - t2;
+    }
+    acc[((c - G.col0) * kMaxChunks + t) * 32 + j] = s;
+}
+
+// plain dot accumulation (used for ||b||^2 before the first iteration)
+__global__ void __launch_bounds__(256) k_dot_acc(CgGeom G, ChunkArg ch,
+                                                 const double *__restrict__ A,
+                                                 const double *__restrict__ B,
+                                                 double *__restrict__ acc) {
+    const int64_t k = G.k;
+    const int64_t c = G.col0 + blockIdx.x * 64 + (threadIdx.x & 63);
+    const int j = __builtin_amdgcn_readfirstlane((int)(blockIdx.y * 4 + (threadIdx.x >> 6)));
+    const int t = blockIdx.z;
+    if (c >= G.col1) return;
+    const int64_t a = ch.a[t], L = ch.len[t];
+    const int64_t n1 = L & ~(int64_t)15, n32 = n1 & ~(int64_t)31;
+    double s = 0.0;
+    for (int64_t row = a + j; row < a + n32; row += 32)
+        s = __builtin_fma(A[row * k + c], B[row * k + c], s);
+    acc[((c - G.col0) * kMaxChunks + t) * 32 + j] = s;
+}
+
+// OpenBLAS ddot finish for one column: 32 chains -> value (see oracle_ddot).
+__device__ double ddot_finish(const double *__restrict__ acc_c, const ChunkArg &ch, int64_t k,
+                              int64_t c, const double *__restrict__ A,
+                              const double *__restrict__ B) {
+    double total = 0.0;
+    for (int t = 0; t < ch.count; ++t) {
+        const int64_t a = ch.a[t], L = ch.len[t];
+        const int64_t n1 = L & ~(int64_t)15, n32 = n1 & ~(int64_t)31;
+        double dot = 0.0;
+        if (n1) {
+            const double *a32 = acc_c + t * 32;
+            double b[16];
+            for (int q = 0; q < 4; ++q)
+                for (int l = 0; l < 4; ++l) b[4 * q + l] = a32[8 * q + l] + a32[8 * q + 4 + l];
+            if (n1 > n32) {
+                for (int jj = 0; jj < 16; ++jj) {
+                    int64_t o = (a + n32 + jj) * k + c;
+                    b[jj] = __builtin_fma(A[o], B[o], b[jj]);
+                }
+            }
+            double c4[4];
+            for (int l = 0; l < 4; ++l) c4[l] = ((b[l] + b[4 + l]) + b[8 + l]) + b[12 + l];
+            dot = (c4[0] + c4[2]) + (c4[1] + c4[3]);
+        }
+        for (int64_t i = a + n1; i < a + L; ++i) {
+            int64_t o = i * k + c;
+            dot = __builtin_fma(B[o], A[o], dot);
+        }
+        if (ch.count == 1) return dot;
+        total = total + dot;
+    }
+    return total;
+}
+
+// init: rho = b.b, bn = sqrt(rho), atol = rtol*bn; bn == 0 -> done (x = b)
+__global__ void k_fin_init(CgGeom G, ChunkArg ch, const double *__restrict__ acc,
+                           const double *__restrict__ Rr, double rtol, double *__restrict__ bn,
+                           double *__restrict__ atol, double *__restrict__ rho,
+                           int32_t *__restrict__ active, int32_t *__restrict__ iters,
+                           int32_t *__restrict__ nactive) {
+    int64_t c = G.col0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (c >= G.col1) return;
+    double d = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.k, c, Rr, Rr);
+    double b = __builtin_sqrt(d);
+    bn[c] = b;
+    double at = rtol * b;  // max(atol=0, rtol*bnrm2)
+    atol[c] = at;
+    rho[c] = d;
+    iters[c] = 0;
+    int act = 1;
+    if (b == 0.0) act = 0;                 // cg returns b, info 0
+    else if (__builtin_sqrt(d) < at) act = 0;  // converged at loop top, iteration 0
+    active[c] = act;
+    if (act) atomicAdd(nactive, 1);
+}
+
+__global__ void k_fin_pq(CgGeom G, ChunkArg ch, const double *__restrict__ acc,
+                         const double *__restrict__ P, const double *__restrict__ Q,
+                         const double *__restrict__ rho, const int32_t *__restrict__ active,
+                         double *__restrict__ alpha) {
+    int64_t c = G.col0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (c >= G.col1 || !active[c]) return;
+    double pq = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.k, c, P, Q);
+    alpha[c] = rho[c] / pq;
+}
+
+// after the update of iteration `it`: rho_prev = rho; rho = r.r; loop-top test
+__global__ void k_fin_rr(CgGeom G, ChunkArg ch, const double *__restrict__ acc,
+                         const double *__restrict__ Rr, int32_t it, double *__restrict__ rho,
+                         double *__restrict__ rho_prev, const double *__restrict__ atol,
+                         int32_t *__restrict__ active, int32_t *__restrict__ iters,
+                         int32_t *__restrict__ nactive) {
+    int64_t c = G.col0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (c >= G.col1 || !active[c]) return;
+    double rr = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.k, c, Rr, Rr);
+    rho_prev[c] = rho[c];
+    rho[c] = rr;
+    iters[c] = it + 1;
+    if (__builtin_sqrt(rr) < atol[c]) {
+        active[c] = 0;
+        atomicSub(nactive, 1);
+    }
+}
+
+// x = b for columns with ||b|| == 0 (cg returns b); zero X elsewhere
+__global__ void k_x_init(CgGeom G, const double *__restrict__ Rr, const double *__restrict__ bn,
+                         double *__restrict__ X) {
+    int64_t ncol = G.col1 - G.col0;
+    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < G.n * ncol;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        int64_t i = idx / ncol, c = G.col0 + idx % ncol;
+        int64_t o = i * G.k + c;
+        X[o] = (bn[c] == 0.0) ? Rr[o] : 0.0;
+    }
+}
+
+// ---------------------------------------------------------------- scores
+// r_eff[e] = 0 + pw_sum_c (Z_u,c - Z_v,c)^2 over columns [col0,col1),
+// Z = nan_to_num(X) (metrics.py:288,292-293); finalize: :296-297.
+__global__ void k_er_scores(const int32_t *__restrict__ rows, const int32_t *__restrict__ ix,
+                            const double *__restrict__ X, int64_t k, int64_t col0, int64_t col1,
+                            int64_t e0, int64_t e1, int finalize, double *__restrict__ out) {
+    for (int64_t e = e0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < e1;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const double *zu = X + (int64_t)rows[e] * k + col0;
+        const double *zv = X + (int64_t)ix[e] * k + col0;
+        double s = pw_sum<double>(col1 - col0, [&](int64_t c) {
+            double a = zu[c], b = zv[c];
+            if (a != a || __builtin_isinf(a)) a = 0.0;
+            if (b != b || __builtin_isinf(b)) b = 0.0;
+            double d = a - b;
+            return d * d;
+        });
+        if (finalize) {
+            s = 0.0 + s;
+            if (s != s || __builtin_isinf(s)) s = 1e-10;
+            s = s > 1e-10 ? s : 1e-10;
+        }
+        out[e - e0] = s;
+    }
+}
+
+static ChunkArg to_arg(const Chunks &c) {
+    ChunkArg a{};
+    a.count = c.count;
+    for (int i = 0; i < c.count; ++i) {
+        a.a[i] = c.a[i];
+        a.len[i] = c.len[i];
+    }
+    return a;
+}
+
+}  // namespace gs
+
+using namespace gs;
+
+extern "C" {
+
+int gs_er_prepare(gs_ctx *c, int64_t k, double reg, int64_t *m_out) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        GS_CHECK(k >= 1, GS_EINVAL, "k must be >= 1");
+        GS_HIP(hipSetDevice(c->device));
+        ensure_transpose(c);
+        Graph &g = c->g;
+        ErState &er = c->er;
+        int64_t n = g.n, nnz = g.nnz;
+        er.n = n;
+        er.k = k;
+        er.proj_next = 0;
+        er.solved = false;
+        // undirected edge ids (u<v in CSR order, metrics.py:236-242)
+        int64_t *eid = (int64_t *)er.edge_id.ensure(sizeof(int64_t) * (nnz ? nnz : 1));
+        int64_t m = 0;
+        if (nnz) {
+            int64_t *flag = (int64_t *)c->scratch[0].ensure(sizeof(int64_t) * nnz);
+            int64_t *pos = (int64_t *)c->scratch[1].ensure(sizeof(int64_t) * nnz);
+            k_upper_flags<<<grid_for(nnz, 256, 8192), 256, 0, c->stream>>>(
+                g.rows.as<int32_t>(), g.indices.as<int32_t>(), nnz, flag);
+            exclusive_scan_i64(c, flag, pos, nnz);
+            k_edge_ids<<<grid_for(nnz, 256, 8192), 256, 0, c->stream>>>(flag, pos, nnz, eid);
+            int64_t last[2];
+            GS_HIP(hipMemcpyAsync(&last[0], pos + nnz - 1, 8, hipMemcpyDeviceToHost, c->stream));
+            GS_HIP(hipMemcpyAsync(&last[1], flag + nnz - 1, 8, hipMemcpyDeviceToHost, c->stream));
+            GS_HIP(hipStreamSynchronize(c->stream));
+            m = last[0] + last[1];
+        }
+        er.m = m;
+        // incidence rows B (metrics.py:260-269)
+        int64_t *cnt = (int64_t *)c->scratch[0].ensure(sizeof(int64_t) * (n + 1));
+        GS_HIP(hipMemsetAsync(cnt, 0, sizeof(int64_t) * (n + 1), c->stream));
+        int64_t *bptr = (int64_t *)er.bptr.ensure(sizeof(int64_t) * (n + 1));
+        if (n)
+            k_b_counts<<<grid_for(n, 256, 8192), 256, 0, c->stream>>>(
+                g.indptr.as<int64_t>(), g.indices.as<int32_t>(), g.tptr.as<int64_t>(),
+                g.tidx.as<int32_t>(), n, cnt);
+        exclusive_scan_i64(c, cnt, bptr, n + 1);
+        er.bcol.ensure(sizeof(int64_t) * (2 * m + 1));
+        er.bsgn.ensure(2 * m + 1);
+        er.bcur.ensure(sizeof(int64_t) * (n + 1));
+        if (n)
+            k_b_fill<<<grid_for(n, 256, 8192), 256, 0, c->stream>>>(
+                g.indptr.as<int64_t>(), g.indices.as<int32_t>(), g.tptr.as<int64_t>(),
+                g.tidx.as<int32_t>(), g.tpos.as<int64_t>(), eid, n, bptr, er.bcol.as<int64_t>(),
+                er.bsgn.as<int8_t>(), er.bcur.as<int64_t>());
+        // L_reg (metrics.py:251-256)
+        GS_HIP(hipMemsetAsync(cnt, 0, sizeof(int64_t) * (n + 1), c->stream));
+        int64_t *lp = (int64_t *)er.lp.ensure(sizeof(int64_t) * (n + 1));
+        if (n)
+            k_l_counts<<<grid_for(n, 256, 8192), 256, 0, c->stream>>>(
+                g.indptr.as<int64_t>(), g.indices.as<int32_t>(), g.data.as<double>(), n, reg, cnt);
+        exclusive_scan_i64(c, cnt, lp, n + 1);
+        int64_t lnnz = 0;
+        GS_HIP(hipMemcpyAsync(&lnnz, lp + n, 8, hipMemcpyDeviceToHost, c->stream));
+        GS_HIP(hipStreamSynchronize(c->stream));
+        er.li.ensure(sizeof(int32_t) * (lnnz + 1));
+        er.lv.ensure(sizeof(double) * (lnnz + 1));
+        if (n)
+            k_l_fill<<<grid_for(n, 256, 8192), 256, 0, c->stream>>>(
+                g.indptr.as<int64_t>(), g.indices.as<int32_t>(), g.data.as<double>(), n, reg, lp,
+                er.li.as<int32_t>(), er.lv.as<double>());
+        // state
+        size_t nk = sizeof(double) * (size_t)(n ? n : 1) * (size_t)k;
+        er.X.ensure(nk);
+        er.Rr.ensure(nk);
+        er.P0.ensure(nk);
+        er.P1.ensure(nk);
+        er.Q.ensure(nk);
+        GS_HIP(hipMemsetAsync(er.Rr.ptr, 0, nk, c->stream));
+        er.colstate.ensure(sizeof(double) * 5 * k + sizeof(int32_t) * (2 * k + 4));
+        GS_HIP(hipMemsetAsync(er.colstate.ptr, 0, er.colstate.bytes, c->stream));
+        er.acc.ensure(sizeof(double) * (size_t)k * kMaxChunks * 32);
+        er.iters.ensure(sizeof(int32_t) * k);
+        GS_HIP(hipStreamSynchronize(c->stream));
+        if (m_out) *m_out = m;
+    });
+}
+
+int gs_er_project_rows(gs_ctx *c, int64_t e0, int64_t e1, const double *raw, int loc,
+                       double sqrt_k) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        ErState &er = c->er;
+        GS_CHECK(er.k > 0, GS_ESTATE, "gs_er_prepare first");
+        GS_CHECK(e0 == er.proj_next && e0 <= e1 && e1 <= er.m, GS_EINVAL,
+                 "rows must be streamed in order: expected %lld, got [%lld, %lld) of %lld",
+                 (long long)er.proj_next, (long long)e0, (long long)e1, (long long)er.m);
+        GS_HIP(hipSetDevice(c->device));
+        int64_t rowsn = e1 - e0;
+        if (rowsn == 0) return;
+        size_t bytes = sizeof(double) * (size_t)rowsn * (size_t)er.k;
+        const double *draw = (const double *)to_device(c, er.rawbuf, raw, bytes, loc);
+        int64_t ncb = (er.k + 63) / 64;
+        hipEvent_t t0 = prof_begin(c);
+        k_project<<<grid_for(er.n * ncb * 64, 256, 65536), 256, 0, c->stream>>>(
+            er.bptr.as<int64_t>(), er.bcol.as<int64_t>(), er.bsgn.as<int8_t>(), er.bcur.as<int64_t>(),
+            er.n, er.k, e0, e1, draw, sqrt_k, er.Rr.as<double>());
+        GS_HIP(hipGetLastError());
+        prof_end(c, t0, "er_project", (double)bytes * 3.0);
+        er.proj_next = e1;
+        if (loc == GS_HOST) GS_HIP(hipStreamSynchronize(c->stream));  // rawbuf reuse
+    });
+}
+
+int gs_er_project_pcg64(gs_ctx *c, uint64_t state_hi, uint64_t state_lo, uint64_t inc_hi,
+                        uint64_t inc_lo, double sqrt_k) {
+    return guard([&] {
+        (void)state_hi; (void)state_lo; (void)inc_hi; (void)inc_lo; (void)sqrt_k;
+        GS_CHECK(c, GS_EINVAL, "null context");
+        GS_CHECK(false, GS_EUNSUPPORTED, "device ziggurat not built in this version");
+    });
+}
+
+int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double rtol,
+                int32_t blas_threads) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        ErState &er = c->er;
+        GS_CHECK(er.k > 0, GS_ESTATE, "gs_er_prepare first");
+        GS_CHECK(er.proj_next == er.m, GS_ESTATE, "projection incomplete: %lld of %lld rows",
+                 (long long)er.proj_next, (long long)er.m);
+        GS_CHECK(0 <= col0 && col0 < col1 && col1 <= er.k, GS_EINVAL, "bad column range");
+        GS_HIP(hipSetDevice(c->device));
+        const int64_t n = er.n, k = er.k;
+        ChunkArg ch = to_arg(make_chunks(n, blas_threads));
+        CgGeom G{n, k, col0, col1};
+        ColPtrs cp = col_ptrs(er);
+        double *X = er.X.as<double>(), *Rr = er.Rr.as<double>(), *Q = er.Q.as<double>();
+        double *P[2] = {er.P0.as<double>(), er.P1.as<double>()};
+        double *acc = er.acc.as<double>();
+        const int64_t ncolb = (col1 - col0 + 63) / 64;
+        dim3 grid((unsigned)ncolb, 8, (unsigned)ch.count), block(256);
+        unsigned fgrid = grid_for(col1 - col0, 64);
+        const double bytes_pq = 32.0 * n * (col1 - col0), bytes_upd = 48.0 * n * (col1 - col0);
+        GS_HIP(hipMemsetAsync(cp.nactive, 0, sizeof(int32_t), c->stream));
+        // ||b|| and rho_0 (r = b.copy())
+        k_dot_acc<<<grid, block, 0, c->stream>>>(G, ch, Rr, Rr, acc);
+        k_fin_init<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Rr, rtol, cp.bn, cp.atol, cp.rho,
+                                                 cp.active, cp.iters, cp.nactive);
+        if (n)
+            k_x_init<<<grid_for(n * (col1 - col0), 256, 65536), 256, 0, c->stream>>>(G, Rr, cp.bn, X);
+        GS_HIP(hipGetLastError());
+        int cur = 0;
+        for (int32_t it = 0; it < maxiter; ++it) {
+            if (it % 8 == 0) {
+                int32_t na = 0;
+                GS_HIP(hipMemcpyAsync(&na, cp.nactive, sizeof(int32_t), hipMemcpyDeviceToHost,
+                                      c->stream));
+                GS_HIP(hipStreamSynchronize(c->stream));
+                if (na == 0) break;
+            }
+            double *Pold = P[cur], *Pnew = P[cur ^ 1];
+            hipEvent_t t0 = prof_begin(c);
+            if (it == 0)
+                k_cg_pq<true><<<grid, block, 0, c->stream>>>(G, ch, er.lp.as<int64_t>(),
+                                                             er.li.as<int32_t>(), er.lv.as<double>(),
+                                                             Rr, Pold, Pnew, Q, cp.rho, cp.rho_prev,
+                                                             cp.active, acc);
+            else
+                k_cg_pq<false><<<grid, block, 0, c->stream>>>(G, ch, er.lp.as<int64_t>(),
+                                                              er.li.as<int32_t>(), er.lv.as<double>(),
+                                                              Rr, Pold, Pnew, Q, cp.rho, cp.rho_prev,
+                                                              cp.active, acc);
+            prof_end(c, t0, "cg_pq", it == 0 ? bytes_pq - 8.0 * n * (col1 - col0) : bytes_pq);
+            k_fin_pq<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Pnew, Q, cp.rho, cp.active, cp.alpha);
+            t0 = prof_begin(c);
+            k_cg_upd<<<grid, block, 0, c->stream>>>(G, ch, Pnew, Q, X, Rr, cp.alpha, cp.active, acc);
+            prof_end(c, t0, "cg_upd", bytes_upd);
+            k_fin_rr<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Rr, it, cp.rho, cp.rho_prev, cp.atol,
+                                                  cp.active, cp.iters, cp.nactive);
+            GS_HIP(hipGetLastError());
+            cur ^= 1;
+        }
+        er.pcur = cur;
+        GS_HIP(hipMemcpyAsync(er.iters.ptr, cp.iters, sizeof(int32_t) * k, hipMemcpyDeviceToDevice,
+                              c->stream));
+        GS_HIP(hipStreamSynchronize(c->stream));
+        er.solved = true;
+    });
+}
+
+int gs_er_scores(gs_ctx *c, int64_t col0, int64_t col1, int64_t e0, int64_t e1, int finalize,
+                 double *out, int loc) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        ErState &er = c->er;
+        GS_CHECK(er.solved, GS_ESTATE, "gs_er_solve first");
+        GS_CHECK(0 <= col0 && col0 <= col1 && col1 <= er.k, GS_EINVAL, "bad column range");
+        GS_CHECK(0 <= e0 && e0 <= e1 && e1 <= c->g.nnz, GS_EINVAL, "bad edge range");
+        GS_HIP(hipSetDevice(c->device));
+        int64_t cnt = e1 - e0;
+        double *dout = (double *)out_device(c, c->outbuf, out, sizeof(double) * cnt, loc);
+        if (cnt) {
+            hipEvent_t t0 = prof_begin(c);
+            k_er_scores<<<grid_for(cnt, 64), 64, 0, c->stream>>>(
+                c->g.rows.as<int32_t>(), c->g.indices.as<int32_t>(), er.X.as<double>(), er.k, col0,
+                col1, e0, e1, finalize, dout);
+            GS_HIP(hipGetLastError());
+            prof_end(c, t0, "er_scores", (16.0 * (col1 - col0) + 16.0) * cnt);
+        }
+        finish_out(c, out, dout, sizeof(double) * cnt, loc);
+    });
+}
+
+int gs_er_iterations(gs_ctx *c, int32_t *iters, int loc) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        ErState &er = c->er;
+        GS_CHECK(er.solved, GS_ESTATE, "gs_er_solve first");
+        GS_HIP(hipMemcpyAsync(iters, er.iters.ptr, sizeof(int32_t) * er.k,
+                              loc == GS_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                              c->stream));
+        GS_HIP(hipStreamSynchronize(c->stream));
+    });
+}
+
+int gs_er_split(int64_t k, int32_t parts, int64_t *bounds) {
+    return guard([&] {
+        GS_CHECK(parts >= 1 && (parts & (parts - 1)) == 0, GS_EINVAL, "parts must be a power of 2");
+        GS_CHECK(bounds, GS_EINVAL, "bounds is NULL");
+        std::vector<int64_t> b = {0, k};
+        for (int32_t p = 1; p < parts; p *= 2) {
+            std::vector<int64_t> nb = {0};
+            for (size_t i = 0; i + 1 < b.size(); ++i) {
+                int64_t lo = b[i], len = b[i + 1] - b[i];
+                GS_CHECK(len > 128, GS_EINVAL,
+                         "k=%lld too small to split %d ways along the pairwise tree",
+                         (long long)k, parts);
+                int64_t n2 = len / 2;
+                n2 -= n2 % 8;
+                nb.push_back(lo + n2);
+                nb.push_back(b[i + 1]);
+            }
+            b.swap(nb);
+        }
+        for (size_t i = 0; i < b.size(); ++i) bounds[i] = b[i];
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,172 @@
+// gs_internal.hpp -- context, device buffers, error plumbing for libgsparse.
+// gfx950 only; compiled with -ffp-contract=off so every product is rounded
+// before it is summed unless a kernel asks for fma() explicitly.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/gsparse.h"
+
+namespace gs {
+
+void set_error(const char *fmt, ...);
+
+struct GsError {
+    int code;
+};
+
+#define GS_HIP(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess) {                                                             \
+            ::gs::set_error("%s:%d %s: %s", __FILE__, __LINE__, #expr, hipGetErrorString(_e)); \
+            throw ::gs::GsError{_e == hipErrorOutOfMemory ? GS_ENOMEM : GS_EHIP};           \
+        }                                                                                   \
+    } while (0)
+
+#define GS_CHECK(cond, code, ...)        \
+    do {                                 \
+        if (!(cond)) {                   \
+            ::gs::set_error(__VA_ARGS__); \
+            throw ::gs::GsError{code};   \
+        }                                \
+    } while (0)
+
+// Grow-only device buffer.
+struct DevBuf {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    void *ensure(size_t n) {
+        if (n <= bytes) return ptr;
+        if (ptr) GS_HIP(hipFree(ptr));
+        ptr = nullptr;
+        bytes = 0;
+        if (n == 0) return nullptr;
+        GS_HIP(hipMalloc(&ptr, n));
+        bytes = n;
+        return ptr;
+    }
+    template <class T>
+    T *as() const { return static_cast<T *>(ptr); }
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+};
+
+struct ProfEntry {
+    int64_t launches = 0;
+    double ms = 0.0;
+    double bytes = 0.0;
+};
+
+struct ProfPending {
+    std::string name;
+    hipEvent_t start, stop;
+    double bytes;
+};
+
+struct Graph {
+    int64_t n = 0, nnz = 0;
+    int symmetric = 0;
+    DevBuf indptr;    // int64 [n+1]
+    DevBuf indices;   // int32 [nnz]
+    DevBuf data;      // f64 [nnz] multiplicity / weight
+    DevBuf rows;      // int32 [nnz] row of each entry
+    DevBuf tptr;      // int64 [n+1] transpose (in-lists), only if !symmetric
+    DevBuf tidx;      // int32 [nnz]
+    DevBuf tpos;      // int64 [nnz] CSR position of each transposed entry
+    bool has_transpose = false;
+};
+
+struct ErState {
+    int64_t k = 0, m = 0, n = 0;
+    int64_t proj_next = 0;  // next R row expected by project_rows
+    DevBuf edge_id;   // int64 [nnz] undirected edge id of CSR entry (u<v), -1 otherwise
+    DevBuf bptr;      // int64 [n+1] incidence rows (B, metrics.py:260-269)
+    DevBuf bcol;      // int64 [2m] edge id (ascending within row)
+    DevBuf bsgn;      // int8  [2m] +1 / -1
+    DevBuf bcur;      // int64 [n] streaming cursor into B rows
+    DevBuf lp, li, lv;  // L_reg CSR (int64, int32, f64)
+    DevBuf X, Rr, P0, P1, Q;  // n x k row-major f64 (Rr starts as Y)
+    DevBuf colstate;  // per-column scalars
+    DevBuf acc;       // dot partial accumulators
+    DevBuf iters;     // int32 [k]
+    DevBuf rawbuf;    // staging for host-streamed raw normals
+    int pcur = 0;     // which of P0/P1 holds the current p
+    bool solved = false;
+};
+
+}  // namespace gs
+
+struct gs_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    bool async_ = false;
+    bool profiling = false;
+    std::map<std::string, gs::ProfEntry> prof;
+    std::vector<std::string> prof_order;
+    std::vector<gs::ProfPending> pending;
+    gs::Graph g;
+    gs::ErState er;
+    gs::DevBuf scratch[6];
+    gs::DevBuf outbuf, inbuf, inbuf2;
+    std::map<std::string, gs::DevBuf> named;  // per-subsystem buffers (backbone, ...)
+    gs::DevBuf &buf(const char *name) { return named[name]; }
+};
+
+namespace gs {
+
+// Record a profiled launch: call prof_begin before the launch and prof_end after.
+hipEvent_t prof_begin(gs_ctx *c);
+void prof_end(gs_ctx *c, hipEvent_t start, const char *name, double bytes);
+void prof_flush(gs_ctx *c);
+void sync_if_needed(gs_ctx *c);
+
+template <class F>
+int guard(F &&f) {
+    try {
+        f();
+        return GS_OK;
+    } catch (const GsError &e) {
+        return e.code;
+    } catch (const std::exception &e) {
+        set_error("std::exception: %s", e.what());
+        return GS_EHIP;
+    } catch (...) {
+        set_error("unknown exception");
+        return GS_EHIP;
+    }
+}
+
+inline unsigned grid_for(int64_t work, int block, int64_t cap = 1 << 20) {
+    int64_t g = (work + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+// Host pointer in -> device copy (staging into buf); device pointer passes through.
+const void *to_device(gs_ctx *c, DevBuf &buf, const void *p, size_t bytes, int loc);
+// Output helper: returns a device pointer to write into; finish_out copies to host if needed.
+void *out_device(gs_ctx *c, DevBuf &buf, void *p, size_t bytes, int loc);
+void finish_out(gs_ctx *c, void *host, const void *dev, size_t bytes, int loc);
+
+// Device-wide helpers (gs_prims.hip)
+void exclusive_scan_i64(gs_ctx *c, const int64_t *in, int64_t *out, int64_t n);
+void sort_keys_u64(gs_ctx *c, uint64_t *keys, int64_t n, int end_bit);
+void sort_pairs_u64_i64(gs_ctx *c, uint64_t *keys, int64_t *vals, int64_t n, int end_bit);
+
+// Graph helpers used by the ER path (gs_graph.hip)
+void ensure_transpose(gs_ctx *c);
+
+}  // namespace gs

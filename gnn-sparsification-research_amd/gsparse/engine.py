@@ -1,0 +1,227 @@
+"""Scorer orchestration over one libgsparse context (host side of the hot path).
+
+Everything numeric runs in libgsparse.so (HIP, gfx950).  The host keeps only
+what the reference defines through NumPy itself and that must therefore be
+evaluated by NumPy to stay bit-identical: the per-node Adamic-Adar weights
+c = 1/sqrt(max(log(deg+1), 1e-10)) (metrics.py:104-108, n values), the JL
+dimension k (metrics.py:248) and -- unless the device ziggurat is selected --
+the PCG64 normal stream R (metrics.py:272), streamed row-chunk by row-chunk.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import queue
+import threading
+
+import numpy as np
+
+from . import _lib
+from ._lib import GS_DEVICE, GS_HOST, Context, ptr
+
+_ROW_CHUNK_BYTES = 64 << 20
+
+
+def blas_threads_default() -> int:
+    """OpenBLAS thread count NumPy would use for np.dot in this process.
+
+    The reference's CG dot products are OpenBLAS ddot calls whose reduction
+    order depends on it (n > 10000); GSPARSE_BLAS_THREADS overrides."""
+    env = os.environ.get("GSPARSE_BLAS_THREADS")
+    if env:
+        return max(1, int(env))
+    try:
+        from threadpoolctl import threadpool_info
+
+        for info in threadpool_info():
+            if info.get("internal_api") == "openblas":
+                return max(1, int(info.get("num_threads", 1)))
+    except Exception:
+        pass
+    env = os.environ.get("OPENBLAS_NUM_THREADS")
+    return max(1, int(env)) if env else 1
+
+
+def jl_dim(n: int, epsilon: float) -> int:
+    """metrics.py:248, evaluated with NumPy exactly as the reference does."""
+    return max(int(24 * np.log(max(n, 2)) / (epsilon ** 2)), 1)
+
+
+def aa_weights(indptr: np.ndarray) -> np.ndarray:
+    """metrics.py:100-108 (adj_binary degrees -> c), NumPy ufuncs as the reference."""
+    degrees = np.diff(indptr).astype(np.float64)
+    log_degrees = np.log(degrees + 1)
+    log_degrees = np.maximum(log_degrees, 1e-10)
+    return 1.0 / np.sqrt(log_degrees)
+
+
+def er_split(k: int, parts: int) -> list[int]:
+    b = np.zeros(parts + 1, dtype=np.int64)
+    _lib.check(_lib.lib().gs_er_split(k, parts, ptr(b)), "gs_er_split")
+    return b.tolist()
+
+
+class Engine:
+    """Scorers over the graph resident in ``ctx``."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self.n, self.nnz, self.symmetric = ctx.shape()
+        self._indptr = None
+
+    # -- helpers ------------------------------------------------------------
+    def indptr(self) -> np.ndarray:
+        if self._indptr is None:
+            ip = np.empty(self.n + 1, dtype=np.int64)
+            self.ctx.call("gs_graph_copy_csr", ptr(ip), None, None, GS_HOST)
+            self._indptr = ip
+        return self._indptr
+
+    def _out(self, e0, e1, out):
+        if out is None:
+            return np.empty(e1 - e0, dtype=np.float64), GS_HOST
+        return out, (GS_HOST if isinstance(out, np.ndarray) else GS_DEVICE)
+
+    # -- scorers ------------------------------------------------------------
+    def jaccard(self, e0: int = 0, e1: int | None = None, out=None):
+        e1 = self.nnz if e1 is None else e1
+        o, loc = self._out(e0, e1, out)
+        self.ctx.call("gs_jaccard", e0, e1, ptr(o), loc)
+        return o
+
+    def adamic_adar(self, e0: int = 0, e1: int | None = None, out=None, c=None):
+        e1 = self.nnz if e1 is None else e1
+        if c is None:
+            c = np.ascontiguousarray(aa_weights(self.indptr()))
+        o, loc = self._out(e0, e1, out)
+        cloc = GS_HOST if isinstance(c, np.ndarray) else GS_DEVICE
+        self.ctx.call("gs_adamic_adar", ptr(c), cloc, e0, e1, ptr(o), loc)
+        return o
+
+    def degree(self, e0: int = 0, e1: int | None = None, out=None):
+        e1 = self.nnz if e1 is None else e1
+        o, loc = self._out(e0, e1, out)
+        self.ctx.call("gs_degree", e0, e1, ptr(o), loc)
+        return o
+
+    def feature_cosine(self, x, e0: int = 0, e1: int | None = None, out=None):
+        """x: (n, f) float32/float64 numpy array or CUDA torch tensor."""
+        e1 = self.nnz if e1 is None else e1
+        if isinstance(x, np.ndarray):
+            xloc = GS_HOST
+            x = np.ascontiguousarray(x)
+            dt = x.dtype
+        else:
+            xloc = GS_DEVICE if x.is_cuda else GS_HOST
+            x = x.contiguous()
+            if xloc == GS_HOST:
+                x = x.numpy()
+                dt = x.dtype
+            else:
+                import torch
+
+                dt = {torch.float32: np.dtype(np.float32),
+                      torch.float64: np.dtype(np.float64)}.get(x.dtype)
+        if x.ndim != 2 or x.shape[0] != self.n:
+            raise ValueError(f"features must be ({self.n}, f), got {tuple(x.shape)}")
+        o, loc = self._out(e0, e1, out)
+        if dt == np.float32:
+            self.ctx.call("gs_feature_cosine_f32", ptr(x), int(x.shape[1]), xloc, e0, e1, ptr(o), loc)
+        elif dt == np.float64:
+            self.ctx.call("gs_feature_cosine_f64", ptr(x), int(x.shape[1]), xloc, e0, e1, ptr(o), loc)
+        else:
+            raise NotImplementedError(f"feature_cosine supports float32/float64 features, got {dt}")
+        return o
+
+    # -- ApproxER -----------------------------------------------------------
+    def er_prepare(self, k: int, reg: float = 1e-6) -> int:
+        m = ctypes.c_int64(0)
+        self.ctx.call("gs_er_prepare", k, reg, ctypes.byref(m))
+        self.k = k
+        self.m = m.value
+        return self.m
+
+    def er_project_host(self, rng: np.random.Generator, k: int):
+        """Stream R = rng.standard_normal((m, k)) row-chunk by row-chunk (identical
+        NumPy stream, verified chunk-invariant) into Y = B @ (R / sqrt(k)),
+        generating chunk i+1 on a worker thread while chunk i is projected."""
+        m = self.m
+        sqrt_k = float(np.sqrt(k))
+        rows = max(1, _ROW_CHUNK_BYTES // (8 * k))
+        q: queue.Queue = queue.Queue(maxsize=2)
+
+        def producer():
+            for e0 in range(0, m, rows):
+                e1 = min(m, e0 + rows)
+                q.put((e0, e1, rng.standard_normal((e1 - e0, k))))
+            q.put(None)
+
+        th = threading.Thread(target=producer, daemon=True)
+        th.start()
+        while True:
+            item = q.get()
+            if item is None:
+                break
+            e0, e1, raw = item
+            self.ctx.call("gs_er_project_rows", e0, e1, ptr(raw), GS_HOST, sqrt_k)
+        th.join()
+
+    def er_project_device(self, rng: np.random.Generator, k: int):
+        st = rng.bit_generator.state
+        if st.get("bit_generator") != "PCG64":
+            raise NotImplementedError("device ziggurat supports the PCG64 bit generator")
+        s, inc = int(st["state"]["state"]), int(st["state"]["inc"])
+        m64 = (1 << 64) - 1
+        if st.get("has_uint32"):
+            raise NotImplementedError("PCG64 state with a buffered uint32")
+        self.ctx.call("gs_er_project_pcg64", s >> 64, s & m64, inc >> 64, inc & m64,
+                      float(np.sqrt(k)))
+
+    def er_solve(self, col0: int, col1: int, maxiter: int, rtol: float, blas_threads: int):
+        self.ctx.call("gs_er_solve", col0, col1, maxiter, rtol, blas_threads)
+
+    def er_scores(self, col0: int, col1: int, finalize: bool = True, e0: int = 0,
+                  e1: int | None = None, out=None):
+        e1 = self.nnz if e1 is None else e1
+        o, loc = self._out(e0, e1, out)
+        self.ctx.call("gs_er_scores", col0, col1, e0, e1, int(finalize), ptr(o), loc)
+        return o
+
+    def er_iterations(self) -> np.ndarray:
+        it = np.empty(self.k, dtype=np.int32)
+        self.ctx.call("gs_er_iterations", ptr(it), GS_HOST)
+        return it
+
+    def approx_er(self, epsilon: float = 0.3, seed: int = 42, max_cg_iters: int = 500,
+                  cg_tol: float = 1e-6, blas_threads: int | None = None,
+                  rng_mode: str | None = None):
+        """calculate_approx_effective_resistance_scores (metrics.py:178-298)."""
+        rng = np.random.default_rng(seed)
+        n = self.n
+        k = jl_dim(n, epsilon)
+        m = self.er_prepare(k)
+        if m == 0:
+            return np.zeros(self.nnz, dtype=np.float64)
+        mode = rng_mode or os.environ.get("GSPARSE_ER_RNG", "host")
+        if mode == "device":
+            self.er_project_device(rng, k)
+        else:
+            self.er_project_host(rng, k)
+        bt = blas_threads_default() if blas_threads is None else blas_threads
+        self.er_solve(0, k, max_cg_iters, cg_tol, bt)
+        return self.er_scores(0, k, True)
+
+    # -- selection ------------------------------------------------------------
+    def topk_mask(self, scores, num_edges: int, num_keep: int, keep_lowest: bool):
+        """Device mask + (cut, #beyond, #tied) -- see gs_topk_mask."""
+        scores = np.ascontiguousarray(scores, dtype=np.float64) if isinstance(scores, np.ndarray) \
+            else scores
+        sloc = GS_HOST if isinstance(scores, np.ndarray) else GS_DEVICE
+        nnz = int(scores.shape[0])
+        mask = np.zeros(num_edges, dtype=np.uint8)
+        cut, nb, nt = ctypes.c_double(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        self.ctx.call("gs_topk_mask", ptr(scores), sloc, nnz, num_edges, num_keep,
+                      int(keep_lowest), ptr(mask), GS_HOST, ctypes.byref(cut), ctypes.byref(nb),
+                      ctypes.byref(nt))
+        return mask.view(bool), cut.value, nb.value, nt.value

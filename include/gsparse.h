@@ -1,0 +1,147 @@
+/*
+ * gsparse.h -- C ABI of libgsparse.so, the MI355X (gfx950) edge-scoring engine.
+ *
+ * This is the drop-in boundary below the reference's Python API
+ * (/root/reference/src/sparsification): the host mirror
+ * gnn-sparsification-research_amd/gsparse/ binds these entry points with
+ * ctypes and keeps the reference's names, argument meaning and error
+ * behaviour.  The reference has no FFI of its own (it is NumPy/SciPy), so
+ * each entry point below cites the reference function whose arithmetic it
+ * replaces.  Conventions:
+ *   - every function returns 0 (GS_OK) or a negative GS_E* code and never
+ *     throws; gs_last_error() gives the message (thread-local);
+ *   - "loc" arguments say where a pointer lives: GS_HOST or GS_DEVICE;
+ *   - scores are float64, one per canonical-CSR entry, in CSR order
+ *     (the reference's adj.nonzero() order, metrics.py:47,115,236,348);
+ *   - calls are synchronous with respect to host pointers; device-pointer
+ *     outputs are complete when the call returns unless gs_set_async(1).
+ */
+#ifndef GSPARSE_H
+#define GSPARSE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_API_VERSION 1
+
+enum {
+    GS_OK = 0,
+    GS_EINVAL = -1,       /* bad argument (Python shim raises ValueError)      */
+    GS_EHIP = -2,         /* HIP runtime error                                 */
+    GS_ENOMEM = -3,       /* device allocation failed                          */
+    GS_ESTATE = -4,       /* call out of order (e.g. no graph set)             */
+    GS_EUNSUPPORTED = -5  /* input outside the implemented contract            */
+};
+
+enum { GS_HOST = 0, GS_DEVICE = 1 };
+
+typedef struct gs_ctx gs_ctx;
+
+/* ---- library / context ------------------------------------------------- */
+int gs_api_version(void);
+const char *gs_last_error(void);
+int gs_device_count(int *count);
+/* One context per (process, device); not re-entrant per context. */
+int gs_create(int device, gs_ctx **out);
+void gs_destroy(gs_ctx *ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream()); NULL =
+ * the context's own stream. */
+int gs_set_stream(gs_ctx *ctx, void *hip_stream);
+int gs_synchronize(gs_ctx *ctx);
+/* 1: device-pointer outputs may still be in flight on return. */
+int gs_set_async(gs_ctx *ctx, int async_);
+
+/* Kernel timing on the context's stream (hipEvents around every launch). */
+int gs_profile_enable(gs_ctx *ctx, int on);
+int gs_profile_reset(gs_ctx *ctx);
+/* i-th profiled kernel name; -1 past the end. ms = summed launch time. */
+int gs_profile_get(gs_ctx *ctx, int i, char *name, int name_len, int64_t *launches,
+                   double *ms, double *bytes);
+
+/* ---- graph --------------------------------------------------------------
+ * Replaces GraphSparsifier.__init__'s COO->CSR build (core.py:70-74):
+ * sp.csr_matrix((ones(E), (ei[0], ei[1])), (n, n)) -- duplicates summed
+ * (data = multiplicity), columns sorted.  Built on the device. */
+int gs_graph_from_edge_index(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src,
+                             const int64_t *dst, int loc);
+/* Canonical CSR given directly (sorted columns, no duplicates), e.g. the
+ * adj argument of the metrics.py module functions. data may be NULL (=1). */
+int gs_graph_from_csr(gs_ctx *ctx, int64_t n, int64_t nnz, const int64_t *indptr,
+                      const int32_t *indices, const double *data, int loc);
+int gs_graph_shape(gs_ctx *ctx, int64_t *n, int64_t *nnz, int *symmetric);
+int gs_graph_copy_csr(gs_ctx *ctx, int64_t *indptr, int32_t *indices, double *data, int loc);
+
+/* ---- scorers: out[e - e0] for CSR entries e in [e0, e1) ------------------ */
+/* calculate_jaccard_scores, metrics.py:17-64 (bit-exact). */
+int gs_jaccard(gs_ctx *ctx, int64_t e0, int64_t e1, double *out, int loc);
+/* calculate_adamic_adar_scores, metrics.py:67-121 (bit-exact).  c[w] =
+ * 1/sqrt(max(log(deg_w+1),1e-10)) as NumPy computes it (metrics.py:104-108),
+ * n values. */
+int gs_adamic_adar(gs_ctx *ctx, const double *c, int c_loc, int64_t e0, int64_t e1,
+                   double *out, int loc);
+/* compute_scores('degree'), core.py:167-172 (bit-exact). */
+int gs_degree(gs_ctx *ctx, int64_t e0, int64_t e1, double *out, int loc);
+/* calculate_feature_cosine_scores, metrics.py:301-358 (bit-exact, x's dtype). */
+int gs_feature_cosine_f32(gs_ctx *ctx, const float *x, int64_t f, int x_loc, int64_t e0,
+                          int64_t e1, double *out, int loc);
+int gs_feature_cosine_f64(gs_ctx *ctx, const double *x, int64_t f, int x_loc, int64_t e0,
+                          int64_t e1, double *out, int loc);
+
+/* ---- ApproxER: calculate_approx_effective_resistance_scores,
+ *      metrics.py:178-298 -------------------------------------------------
+ * gs_er_prepare: edges u<v in CSR order (m of them, :236-242), L_reg =
+ *   diag(rowsum A) - A + reg*I (:251-256); allocates Y/Z (n x k, row-major).
+ * gs_er_project_rows: streams rows [e0, e1) of the raw standard-normal
+ *   matrix (row-major, k per row, NumPy Generator order) and folds
+ *   Y = B @ (raw / sqrt_k) (:272-275) in ascending edge id.  Rows must be
+ *   streamed in order, each exactly once.
+ * gs_er_project_pcg64: the same, drawing the normals on the device from
+ *   NumPy's PCG64 state (state_hi/lo, inc_hi/lo) with NumPy's ziggurat.
+ * gs_er_solve: CG on columns [col0, col1) (:284-289), SciPy 1.15 cg
+ *   recurrence with OpenBLAS-SkylakeX ddot order for blas_threads threads.
+ * gs_er_scores: out[e-e0] = sum over columns [col0,col1) of (Z_u - Z_v)^2 in
+ *   NumPy pairwise order (:292-293).  [col0,col1) must be a node of the
+ *   pairwise tree of k (the whole range, or a gs_er_split() block); when
+ *   finalize != 0 the clamp of :296-297 is applied.
+ * gs_er_iterations: CG iterations each column ran (k values). */
+int gs_er_prepare(gs_ctx *ctx, int64_t k, double reg, int64_t *m_out);
+int gs_er_project_rows(gs_ctx *ctx, int64_t e0, int64_t e1, const double *raw, int loc,
+                       double sqrt_k);
+int gs_er_project_pcg64(gs_ctx *ctx, uint64_t state_hi, uint64_t state_lo, uint64_t inc_hi,
+                        uint64_t inc_lo, double sqrt_k);
+int gs_er_solve(gs_ctx *ctx, int64_t col0, int64_t col1, int32_t maxiter, double rtol,
+                int32_t blas_threads);
+int gs_er_scores(gs_ctx *ctx, int64_t col0, int64_t col1, int64_t e0, int64_t e1,
+                 int finalize, double *out, int loc);
+int gs_er_iterations(gs_ctx *ctx, int32_t *iters, int loc);
+/* Column blocks of the pairwise tree of k at depth log2(parts): bounds has
+ * parts+1 entries.  parts must be a power of two. */
+int gs_er_split(int64_t k, int32_t parts, int64_t *bounds);
+
+/* ---- selection: GraphSparsifier.sparsify core.py:229-242 -----------------
+ * mask[E] (uint8): the num_keep highest (keep_lowest: lowest) of the nnz
+ * scores, ties broken as np.argsort(kind='stable') does (top: highest
+ * indices; lowest: lowest indices); num_keep == 0 keeps all nnz for top
+ * (the reference's idx[-0:] quirk) and none for keep_lowest.  Also returns
+ * the cut key, #strictly-beyond-cut and #tied-at-cut (n_tied > needed means
+ * the reference's unstable argsort may resolve the tie block differently). */
+int gs_topk_mask(gs_ctx *ctx, const double *scores, int s_loc, int64_t nnz, int64_t E,
+                 int64_t num_keep, int keep_lowest, uint8_t *mask, int m_loc,
+                 double *cut, int64_t *n_beyond, int64_t *n_tied);
+
+/* ---- metric backbone: compute_metric_backbone, metric_backbone.py:28-141
+ * keep[idx] for every edge_index column idx=(src,dst): shortest-path
+ * distance d from src in the undirected graph of the src<dst columns
+ * (min weight over duplicates), keep iff d == inf or w[idx] <= d + eps.
+ * n_relax (optional) returns the number of edge relaxations performed. */
+int gs_metric_backbone(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src,
+                       const int64_t *dst, const double *w, int loc, double eps,
+                       uint8_t *keep, int keep_loc, int64_t *n_relax);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSPARSE_H */

@@ -1,0 +1,268 @@
+"""GPU parity: libgsparse.so (through the drop-in API and the C ABI) vs the
+reference's golden vectors and the pinned oracle.
+
+Bar: bit-identical float64 scores for Jaccard / Adamic-Adar / degree /
+FeatCos / ApproxER (the device reproduces NumPy's, SciPy's and OpenBLAS's
+operation order -- golden ApproxER vectors were made with
+OPENBLAS_NUM_THREADS=1, so the device runs with blas_threads=1 here);
+identical keep masks for top-k (numpy tie mode), the metric backbone, the
+sampled and degree-aware selections.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import gsparse_oracle as O
+from conftest import bits_equal, golden_features, golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+
+SMALL = golden_names(include_big=False)
+
+
+@pytest.fixture(scope="module")
+def gs():
+    import gsparse
+
+    return gsparse
+
+
+def make(gs, g, tie_break="numpy", with_x=True):
+    x = golden_features(g) if with_x else None
+    data = gs.Data(edge_index=torch.from_numpy(g["edge_index"]),
+                   x=torch.from_numpy(x) if x is not None else None,
+                   num_nodes=int(g["num_nodes"]))
+    return gs.GraphSparsifier(data, "cpu", tie_break=tie_break), data
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_scores_bit_exact(gs, name):
+    g = load_golden(name)
+    sp_, _ = make(gs, g)
+    a = sp_.adj
+    assert np.array_equal(a.indptr, g["indptr"]) and np.array_equal(a.indices, g["indices"])
+    assert bits_equal(a.data, g["data"])
+    for m in ["jaccard", "adamic_adar", "degree"]:
+        assert bits_equal(sp_.compute_scores(m), g[f"scores_{m}"]), m
+    if "scores_feature_cosine" in g:
+        assert bits_equal(sp_.compute_scores("feature_cosine"), g["scores_feature_cosine"])
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_approx_er_bit_exact(gs, name):
+    g = load_golden(name)
+    sp_, _ = make(gs, g, with_x=False)
+    er = sp_._engine.approx_er(blas_threads=1)
+    ref = g["scores_approx_er"]
+    assert bits_equal(er, ref), float(np.max(np.abs(er - ref) / np.abs(ref)))
+
+
+def test_approx_er_roman_full_bit_exact(gs):
+    """configs[1] size (n=22,662, E=65,854, k=2,674, 500 CG iterations per column)."""
+    g = load_golden("roman_full")
+    sp_, _ = make(gs, g, with_x=False)
+    er = sp_._engine.approx_er(blas_threads=1)
+    ref = g["scores_approx_er"]
+    rel = float(np.max(np.abs(er - ref) / np.abs(ref)))
+    assert rel <= 1e-5, rel  # north_star tolerance
+    assert bits_equal(er, ref), rel
+    it = sp_._engine.er_iterations()
+    assert it.shape == (2674,)
+
+
+def test_roman_full_structural_and_featcos(gs):
+    g = load_golden("roman_full")
+    sp_, _ = make(gs, g)
+    for m in ["jaccard", "adamic_adar", "degree", "feature_cosine"]:
+        assert bits_equal(sp_.compute_scores(m), g[f"scores_{m}"]), m
+
+
+def test_weighted_karate_module_functions(gs):
+    import scipy.sparse as sp
+
+    z = load_golden("karate_weighted")
+    n = int(z["num_nodes"])
+    adj = sp.csr_matrix((z["data"], z["indices"], z["indptr"]), shape=(n, n))
+    assert bits_equal(gs.calculate_jaccard_scores(adj), z["scores_jaccard"])
+    assert bits_equal(gs.calculate_adamic_adar_scores(adj), z["scores_adamic_adar"])
+    er = gs.calculate_approx_effective_resistance_scores(adj, epsilon=0.3, seed=42)
+    assert bits_equal(er, z["scores_approx_er"])
+    from scipy.stats import spearmanr
+
+    assert spearmanr(z["scores_effective_resistance"], er)[0] > 0.5
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_topk_masks(gs, name):
+    g = load_golden(name)
+    sp_n, _ = make(gs, g, "numpy")
+    sp_s, _ = make(gs, g, "stable")
+    metrics = ["jaccard", "adamic_adar", "degree", "approx_er"] + \
+        (["feature_cosine"] if "scores_feature_cosine" in g else [])
+    E = g["edge_index"].shape[1]
+    for m in metrics:
+        sp_n._score_cache[sp_n._normalize_metric_name(m)] = g[f"scores_{m}"]
+        sp_s._score_cache[sp_s._normalize_metric_name(m)] = g[f"scores_{m}"]
+        for r in [0.9, 0.8, 0.6, 0.5, 0.4, 0.2]:
+            for low in (0, 1):
+                _, mask = sp_n.sparsify(m, r, return_mask=True, keep_lowest=bool(low))
+                assert np.array_equal(mask.numpy(), g[f"mask_{m}_{r}_{low}"]), (m, r, low)
+                sd, mask_s = sp_s.sparsify(m, r, return_mask=True, keep_lowest=bool(low))
+                ref_s = O.topk_mask(g[f"scores_{m}"], E, r, bool(low), kind="stable")
+                assert np.array_equal(mask_s.numpy(), ref_s), (m, r, low)
+                assert sd.edge_index.shape[1] == int(mask_s.sum())
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_backbone(gs, name):
+    g = load_golden(name)
+    sp_, data = make(gs, g, with_x=False)
+    for m in ["jaccard", "adamic_adar", "degree", "approx_er"]:
+        cost = g[f"cost_{m}"]
+        if f"backbone_{m}_error" in g:
+            with pytest.raises(IndexError):
+                gs.compute_metric_backbone(data, cost, epsilon=1e-9, verbose=False)
+            continue
+        _, st = gs.compute_metric_backbone(data, cost, epsilon=1e-9, verbose=False)
+        assert np.array_equal(st["keep_mask"], g[f"backbone_{m}"]), m
+        assert st["edges_metric"] == int(g[f"backbone_{m}_metric"])
+
+
+@pytest.mark.parametrize("name", ["karate_test", "roman2000", "cora_like"])
+def test_sampled_degree_aware(gs, name):
+    g = load_golden(name)
+    sp_, _ = make(gs, g, with_x=False)
+    for m in ["jaccard", "degree"]:
+        sp_._score_cache[m] = g[f"scores_{m}"]
+        for r in (0.5, 0.2):
+            _, mk = sp_.sparsify_sampled(m, r, seed=42, return_mask=True)
+            assert np.array_equal(mk.numpy(), g[f"sampled_{m}_{r}"])
+            _, mk = sp_.sparsify_degree_aware(m, r, return_mask=True)
+            assert np.array_equal(mk.numpy(), g[f"degaware_{m}_{r}"])
+
+
+# ----------------------------------------------------------------- larger sizes
+@pytest.fixture(scope="module")
+def rmat14():
+    from gsparse import graphs
+
+    ei = graphs.rmat(14, 8, seed=5)
+    n = 1 << 14
+    ip, ix, d = O.canonical_csr(ei, n)
+    return ei, n, ip, ix, d
+
+
+def test_rmat14_vs_oracle(gs, rmat14):
+    ei, n, ip, ix, d = rmat14
+    data = gs.Data(edge_index=torch.from_numpy(ei), num_nodes=n)
+    sp_ = gs.GraphSparsifier(data, "cpu")
+    assert np.array_equal(sp_.adj.indptr, ip) and np.array_equal(sp_.adj.indices, ix)
+    assert bits_equal(sp_.compute_scores("jaccard"), O.jaccard(ip, ix))
+    assert bits_equal(sp_.compute_scores("adamic_adar"), O.adamic_adar(ip, ix))
+    # edge-range partition (the multi-GPU split) concatenates to the whole
+    e = sp_._engine
+    cuts = [0, 1000, 77777, e.nnz]
+    parts = [e.jaccard(cuts[i], cuts[i + 1]) for i in range(3)]
+    assert bits_equal(np.concatenate(parts), sp_.compute_scores("jaccard"))
+
+
+def test_backbone_rmat12_vs_oracle(gs):
+    from gsparse import graphs
+
+    ei = graphs.rmat(12, 8, seed=2)
+    n = 1 << 12
+    ip, ix, d = O.canonical_csr(ei, n)
+    cost = O.scores_to_cost(O.jaccard(ip, ix), "jaccard")
+    keep_ref = O.metric_backbone(ei, n, cost)
+    data = gs.Data(edge_index=torch.from_numpy(ei), num_nodes=n)
+    _, st = gs.compute_metric_backbone(data, cost, verbose=False)
+    assert np.array_equal(st["keep_mask"], keep_ref)
+
+
+def test_featcos_1433_bow_vs_oracle(gs):
+    from gsparse import graphs
+
+    ei = graphs.chung_lu(2708, 5278, seed=0)
+    x = graphs.features(2708, 1433, seed=1, kind="bow")
+    ip, ix, _ = O.canonical_csr(ei, 2708)
+    data = gs.Data(edge_index=torch.from_numpy(ei), x=torch.from_numpy(x), num_nodes=2708)
+    sp_ = gs.GraphSparsifier(data, "cpu")
+    assert bits_equal(sp_.compute_scores("feature_cosine"), O.feature_cosine(ip, ix, x))
+    x64 = x.astype(np.float64)
+    assert bits_equal(sp_._engine.feature_cosine(x64), O.feature_cosine(ip, ix, x64))
+
+
+def test_topk_large_with_ties_and_specials(gs):
+    rng = np.random.default_rng(0)
+    nnz = 1 << 20
+    s = rng.integers(0, 50, nnz).astype(np.float64) / 7.0  # heavy ties
+    s[::97] = -0.0
+    s[::101] = 0.0
+    s[5] = np.inf
+    s[6] = -np.inf
+    ctx = gs._lib.Context()
+    ctx.set_graph_csr(2, np.array([0, 1, 2]), np.array([1, 0], dtype=np.int32), None)
+    eng = gs.engine.Engine(ctx)
+    for frac in [0.001, 0.3, 0.5, 0.999]:
+        for low in (False, True):
+            k = int(nnz * frac)
+            mask, cut, nb, nt = eng.topk_mask(s, nnz + 5, k, low)
+            ref = O.topk_mask(s, nnz + 5, frac, low, kind="stable")
+            if int((nnz + 5) * frac) != k:
+                ref = np.zeros(nnz + 5, dtype=bool)
+                idx = np.argsort(s, kind="stable")
+                ref[idx[:k] if low else idx[-k:]] = True
+            assert np.array_equal(mask, ref), (frac, low)
+            assert mask.sum() == k
+    # quirks: num_keep 0 keeps every scored column (idx[-0:]), keep_lowest keeps none
+    m0, *_ = eng.topk_mask(s, nnz + 5, 0, False)
+    assert m0[:nnz].all() and not m0[nnz:].any()
+    m1, *_ = eng.topk_mask(s, nnz + 5, 0, True)
+    assert not m1.any()
+
+
+def test_edge_cases(gs):
+    # isolated nodes, single edge, empty graph, self-loops + duplicates
+    for ei, n in [(np.array([[0, 1], [1, 0]]), 5), (np.zeros((2, 0), dtype=np.int64), 3),
+                  (np.array([[0, 0, 1, 1, 2, 2], [0, 1, 0, 0, 2, 1]]), 3)]:
+        data = gs.Data(edge_index=torch.from_numpy(ei.astype(np.int64)), num_nodes=n)
+        sp_ = gs.GraphSparsifier(data, "cpu")
+        ip, ix, d = O.canonical_csr(ei, n)
+        assert bits_equal(sp_.compute_scores("jaccard"), O.jaccard(ip, ix))
+        assert bits_equal(sp_.compute_scores("adamic_adar"), O.adamic_adar(ip, ix))
+        assert bits_equal(sp_.compute_scores("degree"), O.degree(ip, ix, d))
+        er = sp_._engine.approx_er(blas_threads=1)
+        assert bits_equal(er, O.approx_er(ip, ix, d, n, impl="c"))
+
+
+def test_errors_mirror_reference(gs):
+    g = load_golden("karate_test")
+    sp_, _ = make(gs, g, with_x=False)
+    with pytest.raises(ValueError, match="not supported"):
+        sp_.compute_scores("pagerank")
+    for bad in (0, -0.1, 1.5):
+        with pytest.raises(ValueError, match="retention_ratio"):
+            sp_.sparsify("jaccard", bad)
+    with pytest.raises(ValueError, match="requires node features"):
+        sp_.compute_scores("feature_cosine")
+    d, m = sp_.sparsify("jaccard", 1.0, return_mask=True)
+    assert m.all() and d.edge_index.shape[1] == 156
+    assert sp_.sparsify("jaccard", 0.5).edge_index.size(1) == 78
+
+
+def test_er_column_split_combines_to_whole(gs):
+    """Multi-GPU ApproxER split (pairwise-tree column blocks) is exact on one device."""
+    g = load_golden("rmat10")
+    sp_, _ = make(gs, g, with_x=False)
+    e = sp_._engine
+    full = e.approx_er(blas_threads=1)
+    k = e.k
+    for parts in (2, 4):
+        b = gs.engine.er_split(k, parts)
+        sums = [e.er_scores(b[i], b[i + 1], finalize=False) for i in range(parts)]
+        while len(sums) > 1:
+            sums = [sums[i] + sums[i + 1] for i in range(0, len(sums), 2)]
+        tot = 0.0 + sums[0]
+        tot = np.maximum(np.nan_to_num(tot, nan=1e-10, posinf=1e-10, neginf=1e-10), 1e-10)
+        assert bits_equal(tot, full)

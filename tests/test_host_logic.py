@@ -1,0 +1,123 @@
+"""Host logic of the drop-in API that needs no GPU.
+
+Metric-name normalisation, the cost transform, the NumPy-defined selection
+helpers (sampled / degree-aware), the Data stand-in, the synthetic graph
+generators, the JL dimension and the Adamic-Adar weight table -- each
+checked against the reference's golden vectors or its documented answers.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import gsparse_oracle as O
+from conftest import golden_names, load_golden
+from gsparse import graphs
+from gsparse.core import GraphSparsifier
+from gsparse.data import Data
+from gsparse.engine import aa_weights, jl_dim
+from gsparse.selection import degree_aware_mask, numpy_topk_mask, sampled_mask
+
+SMALL = golden_names(include_big=False)
+
+
+def bare_sparsifier():
+    return GraphSparsifier.__new__(GraphSparsifier)
+
+
+def test_normalize_metric_names():
+    s = bare_sparsifier()
+    cases = {"jaccard": "jaccard", "Adamic-Adar": "adamic_adar", "aa": "adamic_adar",
+             "ER": "effective_resistance", "effective-resistance": "effective_resistance",
+             "approx_er": "approx_effective_resistance", "rand": "random",
+             "degree": "degree", "Feature Cosine": "feature_cosine",
+             "feature-cosine": "feature_cosine"}
+    for k, v in cases.items():
+        assert s._normalize_metric_name(k) == v
+    with pytest.raises(ValueError, match="not supported"):
+        s._normalize_metric_name("pagerank")
+
+
+def test_scores_to_cost_known_answer():
+    # tests/test_sparsification.py:143-150
+    s = bare_sparsifier()
+    np.testing.assert_allclose(s._scores_to_cost(np.array([0.5, 1.0, 0.25]), "jaccard"),
+                               [1.0, 0.0, 3.0])
+    assert np.all(s._scores_to_cost(np.zeros(4), "jaccard") == 1.0)
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_scores_to_cost_matches_golden(name):
+    g = load_golden(name)
+    s = bare_sparsifier()
+    for m in ["jaccard", "adamic_adar", "degree", "approx_er"]:
+        c = s._scores_to_cost(g[f"scores_{m}"], m)
+        assert np.array_equal(c.view(np.uint64), g[f"cost_{m}"].view(np.uint64))
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_sampled_and_degree_aware_match_golden(name):
+    g = load_golden(name)
+    E = g["edge_index"].shape[1]
+    n = int(g["num_nodes"])
+    for m in ["jaccard", "adamic_adar", "degree", "approx_er", "feature_cosine"]:
+        if f"scores_{m}" not in g:
+            continue
+        s = g[f"scores_{m}"]
+        for r in (0.5, 0.2):
+            if f"sampled_{m}_{r}" in g:
+                assert np.array_equal(sampled_mask(s, E, r, 42), g[f"sampled_{m}_{r}"])
+            elif f"sampled_{m}_{r}_error" in g:
+                with pytest.raises(ValueError):
+                    sampled_mask(s, E, r, 42)
+            if f"degaware_{m}_{r}" in g:
+                got = degree_aware_mask(s, g["edge_index"], n, E, r)
+                assert np.array_equal(got, g[f"degaware_{m}_{r}"]), (m, r)
+            elif f"degaware_{m}_{r}_error" in g:
+                with pytest.raises(IndexError):
+                    degree_aware_mask(s, g["edge_index"], n, E, r)
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_numpy_topk_mask_is_reference(name):
+    g = load_golden(name)
+    E = g["edge_index"].shape[1]
+    for r in [0.9, 0.5, 0.2]:
+        for low in (0, 1):
+            got = numpy_topk_mask(g["scores_jaccard"], E, int(E * r), bool(low))
+            assert np.array_equal(got, g[f"mask_jaccard_{r}_{low}"])
+
+
+def test_aa_weights_and_jl_dim():
+    g = load_golden("rmat10")
+    assert np.array_equal(aa_weights(g["indptr"]), O.aa_weights(g["indptr"]))
+    assert jl_dim(22662, 0.3) == 2674
+    assert jl_dim(2708, 0.3) == 2107
+    assert jl_dim(1, 0.3) == jl_dim(2, 0.3)
+    assert jl_dim(169343, 0.3) == 3210
+
+
+def test_data_standin():
+    ei = torch.tensor([[0, 1], [1, 0]])
+    d = Data(edge_index=ei, num_nodes=3, y=torch.zeros(3))
+    assert d.num_nodes == 3
+    c = d.clone()
+    c.edge_index[0, 0] = 7
+    assert d.edge_index[0, 0] == 0
+    assert d.to("cpu").y.shape == (3,)
+    assert Data(edge_index=ei).num_nodes == 2
+
+
+def test_generators_are_deterministic_and_canonical():
+    a = graphs.roman_like(2000, 2906, seed=3)
+    b = graphs.roman_like(2000, 2906, seed=3)
+    assert np.array_equal(a, b)
+    assert a.shape == (2, 2 * 2906)
+    keys = a[0] * 2000 + a[1]
+    assert np.all(np.diff(keys) > 0)  # row-major sorted, duplicate free
+    rev = np.sort(a[1] * 2000 + a[0])
+    assert np.array_equal(np.sort(keys), rev)  # symmetric
+    r = graphs.rmat(10, 16, seed=1)
+    assert np.array_equal(r, load_golden("rmat10")["edge_index"])
+    full = graphs.roman_like()
+    assert full.shape == (2, 65854)
