@@ -223,8 +223,17 @@ __global__ void __launch_bounds__(256) k_project(const int64_t *__restrict__ bpt
     for (int64_t w = wave; w < n * ncb; w += nwaves) {
         int64_t i = w / ncb, cb = w % ncb;
         int64_t c = cb * 64 + lane;
-        int64_t cur = bcur[i], end = bptr[i + 1];
-        int64_t p = cur;
+        // first incident edge id >= e0 (B rows are sorted): stateless, so the
+        // column slices of one node need no shared cursor
+        int64_t p = bptr[i], end = bptr[i + 1];
+        {
+            int64_t hi = end;
+            while (p < hi) {
+                int64_t mid = (p + hi) >> 1;
+                if (bcol[mid] < e0) p = mid + 1;
+                else hi = mid;
+            }
+        }
         double y = (c < k) ? Y[i * k + c] : 0.0;
         for (; p < end; ++p) {
             int64_t e = bcol[p];
@@ -236,8 +245,8 @@ __global__ void __launch_bounds__(256) k_project(const int64_t *__restrict__ bpt
             }
         }
         if (c < k) Y[i * k + c] = y;
-        if (cb == ncb - 1 && lane == 0) bcur[i] = p;  // last slice advances the cursor
     }
+    (void)bcur;
 }
 
 // ---------------------------------------------------------------- CG kernels
