@@ -98,7 +98,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--blas-threads", type=int, default=8,
                     help="OpenBLAS ddot order to reproduce (reference run with this many threads)")
-    ap.add_argument("--rng", default=os.environ.get("GSPARSE_ER_RNG", "host"),
+    ap.add_argument("--rng", default=os.environ.get("GSPARSE_ER_RNG", "device"),
                     choices=["host", "device"])
     ap.add_argument("--cpu-sample-cols", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -641,15 +641,6 @@ int gs_er_project_rows(gs_ctx *c, int64_t e0, int64_t e1, const double *raw, int
     });
 }
 
-int gs_er_project_pcg64(gs_ctx *c, uint64_t state_hi, uint64_t state_lo, uint64_t inc_hi,
-                        uint64_t inc_lo, double sqrt_k) {
-    return guard([&] {
-        (void)state_hi; (void)state_lo; (void)inc_hi; (void)inc_lo; (void)sqrt_k;
-        GS_CHECK(c, GS_EINVAL, "null context");
-        GS_CHECK(false, GS_EUNSUPPORTED, "device ziggurat not built in this version");
-    });
-}
-
 int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double rtol,
                 int32_t blas_threads) {
     return guard([&] {

@@ -203,7 +203,7 @@ class Engine:
         m = self.er_prepare(k)
         if m == 0:
             return np.zeros(self.nnz, dtype=np.float64)
-        mode = rng_mode or os.environ.get("GSPARSE_ER_RNG", "host")
+        mode = rng_mode or os.environ.get("GSPARSE_ER_RNG", "device")
         if mode == "device":
             self.er_project_device(rng, k)
         else:

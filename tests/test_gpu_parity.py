@@ -266,3 +266,20 @@ def test_er_column_split_combines_to_whole(gs):
         tot = 0.0 + sums[0]
         tot = np.maximum(np.nan_to_num(tot, nan=1e-10, posinf=1e-10, neginf=1e-10), 1e-10)
         assert bits_equal(tot, full)
+
+
+# ------------------------------------------------------ device normal stream
+@pytest.mark.parametrize("name", SMALL)
+def test_approx_er_device_rng_bit_exact(gs, name):
+    """R drawn on the device (PCG64 + NumPy's ziggurat) -> identical scores."""
+    g = load_golden(name)
+    sp_, _ = make(gs, g, with_x=False)
+    er = sp_._engine.approx_er(blas_threads=1, rng_mode="device")
+    assert bits_equal(er, g["scores_approx_er"])
+
+
+def test_approx_er_device_rng_roman_full(gs):
+    g = load_golden("roman_full")
+    sp_, _ = make(gs, g, with_x=False)
+    er = sp_._engine.approx_er(blas_threads=1, rng_mode="device")
+    assert bits_equal(er, g["scores_approx_er"])
