@@ -207,13 +207,12 @@ __global__ void k_l_fill(const int64_t *__restrict__ ip, const int32_t *__restri
 // ---------------------------------------------------------------- projection
 // Y[i,:] += sign * raw[e - e0, :] / sqrt_k for node i's incident edges e in
 // [e0, e1), in ascending e (metrics.py:272-275; SciPy csr_matvecs folds B's
-// sorted row from 0.0, +-1 * R exact).  One block (64 lanes) per node and
-// 64-column slice.
+// sorted row from 0.0, +-1 * R exact).  One wave per node and 64-column
+// slice.  raw is row-major with stride k (NumPy layout); Y has stride ld.
 __global__ void __launch_bounds__(256) k_project(const int64_t *__restrict__ bptr,
                                                  const int64_t *__restrict__ bcol,
-                                                 const int8_t *__restrict__ bsgn,
-                                                 int64_t *__restrict__ bcur, int64_t n, int64_t k,
-                                                 int64_t e0, int64_t e1,
+                                                 const int8_t *__restrict__ bsgn, int64_t n,
+                                                 int64_t k, int64_t ld, int64_t e0, int64_t e1,
                                                  const double *__restrict__ raw, double sqrt_k,
                                                  double *__restrict__ Y) {
     int64_t ncb = (k + 63) / 64;
@@ -234,7 +233,7 @@ __global__ void __launch_bounds__(256) k_project(const int64_t *__restrict__ bpt
                 else hi = mid;
             }
         }
-        double y = (c < k) ? Y[i * k + c] : 0.0;
+        double y = (c < k) ? Y[i * ld + c] : 0.0;
         for (; p < end; ++p) {
             int64_t e = bcol[p];
             if (e >= e1) break;
@@ -244,9 +243,8 @@ __global__ void __launch_bounds__(256) k_project(const int64_t *__restrict__ bpt
                 y = y + t;
             }
         }
-        if (c < k) Y[i * k + c] = y;
+        if (c < k) Y[i * ld + c] = y;
     }
-    (void)bcur;
 }
 
 // ---------------------------------------------------------------- CG kernels
@@ -256,19 +254,63 @@ struct ChunkArg {
     int64_t len[kMaxChunks];
 };
 
-// Grid: x = column blocks of 64, y = residue groups (4 per block -> 8 groups
-// cover j = 0..31), z = chunk.  Block = 256 threads = 4 waves; wave w holds
-// residue j = 4*blockIdx.y + w for 64 consecutive columns (512-B coalesced rows).
+// Geometry of one batched-CG launch.  Lane layout: a wave owns ONE residue
+// j (rows j, j+32, ... of a BLAS chunk -- that row sequence IS the OpenBLAS
+// accumulator chain j) for CPL*64 consecutive columns, CPL columns per lane
+// (CPL=2: 16-byte loads, two independent chains per lane).  A 256-thread
+// workgroup holds 4 residues; the 8 workgroups of one (column block, chunk)
+// pair get block ids b, b+8, ..., b+56 -- under the round-robin dispatch over
+// the 8 XCDs they share one XCD's L2, so the neighbour rows a chain's SpMV
+// gathers (mostly rows i-1, i+1, i+chord: other residues) are L2 hits.
 struct CgGeom {
-    int64_t n, k, col0, col1;
+    int64_t n, k, ld, col0, col1;
+    int32_t ncb;     // column blocks of CPL*64
+    int32_t npairs;  // ncb * chunks
 };
 
-__device__ __forceinline__ int64_t wave_uniform(int64_t v) {
-    return ((int64_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
-           (uint32_t)__builtin_amdgcn_readfirstlane((int)(v & 0xffffffff));
+struct CgLane {
+    int64_t c;   // first column of this lane
+    int j, t;    // residue, chunk
+    bool ok;
+};
+
+template <int CPL>
+__device__ __forceinline__ CgLane cg_lane(const CgGeom &G) {
+    const int b = blockIdx.x;
+    const int grp = b >> 6, r = b & 63;
+    const int sub = r & 7, part = r >> 3;  // part: which 4 of the 32 residues
+    const int pair = grp * 8 + sub;
+    CgLane L;
+    L.ok = pair < G.npairs;
+    const int cb = pair % G.ncb;
+    L.t = pair / G.ncb;
+    L.j = __builtin_amdgcn_readfirstlane(part * 4 + (int)(threadIdx.x >> 6));
+    L.c = G.col0 + (int64_t)cb * (64 * CPL) + (int64_t)(threadIdx.x & 63) * CPL;
+    return L;
 }
 
-template <bool FIRST>
+template <int CPL>
+struct Vec;
+template <>
+struct Vec<1> {
+    double v[1];
+    __device__ __forceinline__ void load(const double *p) { v[0] = *p; }
+    __device__ __forceinline__ void store(double *p) const { *p = v[0]; }
+};
+template <>
+struct Vec<2> {
+    double v[2];
+    __device__ __forceinline__ void load(const double *p) {
+        double2 t = *reinterpret_cast<const double2 *>(p);
+        v[0] = t.x;
+        v[1] = t.y;
+    }
+    __device__ __forceinline__ void store(double *p) const {
+        *reinterpret_cast<double2 *>(p) = make_double2(v[0], v[1]);
+    }
+};
+
+template <bool FIRST, int CPL>
 __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
                                                const int64_t *__restrict__ lp,
                                                const int32_t *__restrict__ li,
@@ -280,68 +322,97 @@ __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
                                                const double *__restrict__ rho_prev,
                                                const int32_t *__restrict__ active,
                                                double *__restrict__ acc) {
-    const int64_t k = G.k;
-    const int64_t c = G.col0 + blockIdx.x * 64 + (threadIdx.x & 63);
-    const int j = __builtin_amdgcn_readfirstlane((int)(blockIdx.y * 4 + (threadIdx.x >> 6)));
-    const int t = blockIdx.z;
-    const bool live = c < G.col1 && active[c];
-    double beta = 0.0;
-    if (!FIRST && live) beta = rho[c] / rho_prev[c];
-    const int64_t a = ch.a[t], L = ch.len[t];
+    const CgLane ln = cg_lane<CPL>(G);
+    if (!ln.ok) return;
+    const int64_t ld = G.ld, c = ln.c;
+    bool live[CPL];
+    double beta[CPL];
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+        live[u] = (c + u) < G.col1 && active[c + u];
+        beta[u] = (!FIRST && live[u]) ? rho[c + u] / rho_prev[c + u] : 0.0;
+        any = any || live[u];
+    }
+    if (!any) return;
+    const int64_t a = ch.a[ln.t], L = ch.len[ln.t];
     const int64_t n1 = L & ~(int64_t)15, n32 = n1 & ~(int64_t)31;
-    double s = 0.0;
-    auto pnew = [&](int64_t row) -> double {
-        double r = R[row * k + c];
-        if (FIRST) return r;
-        double pb = Pold[row * k + c] * beta;
-        return pb + r;
-    };
-    if (!live) return;
-    // main region: rows a + j + 32 s, FMA chain
-    for (int64_t row = a + j; row < a + n32; row += 32) {
-        int64_t e0 = lp[row], e1 = lp[row + 1];
-        double q = 0.0, pi = 0.0;
+    double s[CPL];
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) s[u] = 0.0;
+
+    auto row_pq = [&](int64_t row, double *pi, double *q) {
+        const int64_t e0 = lp[row], e1 = lp[row + 1];
         bool found = false;
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            q[u] = 0.0;
+            pi[u] = 0.0;
+        }
         for (int64_t e = e0; e < e1; ++e) {
-            int32_t col = li[e];
-            double pv = pnew(col);
-            if (col == row) {
-                pi = pv;
-                found = true;
-            }
-            double prod = lv[e] * pv;
-            q = q + prod;
-        }
-        if (!found) pi = pnew(row);
-        Pnew[row * k + c] = pi;
-        Q[row * k + c] = q;
-        s = __builtin_fma(pi, q, s);
-    }
-    // leftover rows of the chunk (16-block + tail): computed, not accumulated
-    {
-        int64_t row = a + n32 + j;
-        if (row < a + L) {
-            int64_t e0 = lp[row], e1 = lp[row + 1];
-            double q = 0.0, pi = 0.0;
-            bool found = false;
-            for (int64_t e = e0; e < e1; ++e) {
-                int32_t col = li[e];
-                double pv = pnew(col);
-                if (col == row) {
-                    pi = pv;
-                    found = true;
+            const int32_t col = li[e];
+            const double w = lv[e];
+            Vec<CPL> rv, pv;
+            rv.load(R + col * ld + c);
+            if (!FIRST) pv.load(Pold + col * ld + c);
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                double pn;
+                if (FIRST) {
+                    pn = rv.v[u];
+                } else {
+                    double pb = pv.v[u] * beta[u];
+                    pn = pb + rv.v[u];
                 }
-                double prod = lv[e] * pv;
-                q = q + prod;
+                if (col == row) pi[u] = pn;
+                double prod = w * pn;
+                q[u] = q[u] + prod;
             }
-            if (!found) pi = pnew(row);
-            Pnew[row * k + c] = pi;
-            Q[row * k + c] = q;
+            found = found || (col == row);
+        }
+        if (!found) {  // L_reg_ii dropped (== 0): p_i still needed
+            Vec<CPL> rv, pv;
+            rv.load(R + row * ld + c);
+            if (!FIRST) pv.load(Pold + row * ld + c);
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                if (FIRST) {
+                    pi[u] = rv.v[u];
+                } else {
+                    double pb = pv.v[u] * beta[u];
+                    pi[u] = pb + rv.v[u];
+                }
+            }
+        }
+        Vec<CPL> po, qo;
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            po.v[u] = pi[u];
+            qo.v[u] = q[u];
+        }
+        po.store(Pnew + row * ld + c);
+        qo.store(Q + row * ld + c);
+    };
+
+    for (int64_t row = a + ln.j; row < a + n32; row += 32) {
+        double pi[CPL], q[CPL];
+        row_pq(row, pi, q);
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) s[u] = __builtin_fma(pi[u], q[u], s[u]);
+    }
+    {  // leftover rows of the chunk (16-block + tail): computed, not accumulated
+        const int64_t row = a + n32 + ln.j;
+        if (row < a + L) {
+            double pi[CPL], q[CPL];
+            row_pq(row, pi, q);
         }
     }
-    acc[((c - G.col0) * kMaxChunks + t) * 32 + j] = s;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u)
+        if (c + u < G.col1) acc[((c + u - G.col0) * kMaxChunks + ln.t) * 32 + ln.j] = s[u];
 }
 
+template <int CPL>
 __global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
                                                 const double *__restrict__ P,
                                                 const double *__restrict__ Q,
@@ -349,56 +420,99 @@ __global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
                                                 const double *__restrict__ alpha,
                                                 const int32_t *__restrict__ active,
                                                 double *__restrict__ acc) {
-    const int64_t k = G.k;
-    const int64_t c = G.col0 + blockIdx.x * 64 + (threadIdx.x & 63);
-    const int j = __builtin_amdgcn_readfirstlane((int)(blockIdx.y * 4 + (threadIdx.x >> 6)));
-    const int t = blockIdx.z;
-    if (!(c < G.col1 && active[c])) return;
-    const double al = alpha[c];
-    const int64_t a = ch.a[t], L = ch.len[t];
+    const CgLane ln = cg_lane<CPL>(G);
+    if (!ln.ok) return;
+    const int64_t ld = G.ld, c = ln.c;
+    double al[CPL];
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+        bool live = (c + u) < G.col1 && active[c + u];
+        al[u] = live ? alpha[c + u] : 0.0;
+        any = any || live;
+    }
+    if (!any) return;
+    const int64_t a = ch.a[ln.t], L = ch.len[ln.t];
     const int64_t n1 = L & ~(int64_t)15, n32 = n1 & ~(int64_t)31;
-    double s = 0.0;
-    for (int64_t row = a + j; row < a + n32; row += 32) {
-        int64_t o = row * k + c;
-        double t1 = al * P[o];
-        double x = X[o] + t1;
-        double t2 = al * Q[o];
-        double r = R[o] - t2;
-        X[o] = x;
-        R[o] = r;
-        s = __builtin_fma(r, r, s);
+    double s[CPL];
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) s[u] = 0.0;
+    auto upd = [&](int64_t row, Vec<CPL> &rv) {
+        const int64_t o = row * ld + c;
+        Vec<CPL> xv, pv, qv;
+        xv.load(X + o);
+        pv.load(P + o);
+        qv.load(Q + o);
+        rv.load(R + o);
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            double t1 = al[u] * pv.v[u];
+            xv.v[u] = xv.v[u] + t1;
+            double t2 = al[u] * qv.v[u];
+            rv.v[u] = rv.v[u] - t2;
+        }
+        xv.store(X + o);
+        rv.store(R + o);
+    };
+    int64_t row = a + ln.j;
+    const int64_t end = a + n32;
+    // two rows per trip: both rows' loads are in flight before either FMA
+    for (; row + 32 < end; row += 64) {
+        Vec<CPL> r0, r1;
+        upd(row, r0);
+        upd(row + 32, r1);
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            s[u] = __builtin_fma(r0.v[u], r0.v[u], s[u]);
+            s[u] = __builtin_fma(r1.v[u], r1.v[u], s[u]);
+        }
     }
-    int64_t row = a + n32 + j;
-    if (row < a + L) {
-        int64_t o = row * k + c;
-        double t1 = al * P[o];
-        double t2 = al * Q[o];
-        X[o] = X[o] + t1;
-        R[o] = R[o] - t2;
+    for (; row < end; row += 32) {
+        Vec<CPL> r0;
+        upd(row, r0);
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) s[u] = __builtin_fma(r0.v[u], r0.v[u], s[u]);
     }
-    acc[((c - G.col0) * kMaxChunks + t) * 32 + j] = s;
+    {
+        const int64_t lrow = a + n32 + ln.j;
+        if (lrow < a + L) {
+            Vec<CPL> r0;
+            upd(lrow, r0);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < CPL; ++u)
+        if (c + u < G.col1) acc[((c + u - G.col0) * kMaxChunks + ln.t) * 32 + ln.j] = s[u];
 }
 
-// plain dot accumulation (used for ||b||^2 before the first iteration)
+// plain dot accumulation (||b||^2 before the first iteration)
+template <int CPL>
 __global__ void __launch_bounds__(256) k_dot_acc(CgGeom G, ChunkArg ch,
                                                  const double *__restrict__ A,
                                                  const double *__restrict__ B,
                                                  double *__restrict__ acc) {
-    const int64_t k = G.k;
-    const int64_t c = G.col0 + blockIdx.x * 64 + (threadIdx.x & 63);
-    const int j = __builtin_amdgcn_readfirstlane((int)(blockIdx.y * 4 + (threadIdx.x >> 6)));
-    const int t = blockIdx.z;
-    if (c >= G.col1) return;
-    const int64_t a = ch.a[t], L = ch.len[t];
+    const CgLane ln = cg_lane<CPL>(G);
+    if (!ln.ok) return;
+    const int64_t ld = G.ld, c = ln.c;
+    const int64_t a = ch.a[ln.t], L = ch.len[ln.t];
     const int64_t n1 = L & ~(int64_t)15, n32 = n1 & ~(int64_t)31;
-    double s = 0.0;
-    for (int64_t row = a + j; row < a + n32; row += 32)
-        s = __builtin_fma(A[row * k + c], B[row * k + c], s);
-    acc[((c - G.col0) * kMaxChunks + t) * 32 + j] = s;
+    double s[CPL];
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) s[u] = 0.0;
+    for (int64_t row = a + ln.j; row < a + n32; row += 32) {
+        Vec<CPL> av, bv;
+        av.load(A + row * ld + c);
+        bv.load(B + row * ld + c);
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) s[u] = __builtin_fma(av.v[u], bv.v[u], s[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < CPL; ++u)
+        if (c + u < G.col1) acc[((c + u - G.col0) * kMaxChunks + ln.t) * 32 + ln.j] = s[u];
 }
 
 // OpenBLAS ddot finish for one column: 32 chains -> value (see oracle_ddot).
-__device__ double ddot_finish(const double *__restrict__ acc_c, const ChunkArg &ch, int64_t k,
+__device__ double ddot_finish(const double *__restrict__ acc_c, const ChunkArg &ch, int64_t ld,
                               int64_t c, const double *__restrict__ A,
                               const double *__restrict__ B) {
     double total = 0.0;
@@ -413,7 +527,7 @@ __device__ double ddot_finish(const double *__restrict__ acc_c, const ChunkArg &
                 for (int l = 0; l < 4; ++l) b[4 * q + l] = a32[8 * q + l] + a32[8 * q + 4 + l];
             if (n1 > n32) {
                 for (int jj = 0; jj < 16; ++jj) {
-                    int64_t o = (a + n32 + jj) * k + c;
+                    int64_t o = (a + n32 + jj) * ld + c;
                     b[jj] = __builtin_fma(A[o], B[o], b[jj]);
                 }
             }
@@ -422,7 +536,7 @@ __device__ double ddot_finish(const double *__restrict__ acc_c, const ChunkArg &
             dot = (c4[0] + c4[2]) + (c4[1] + c4[3]);
         }
         for (int64_t i = a + n1; i < a + L; ++i) {
-            int64_t o = i * k + c;
+            int64_t o = i * ld + c;
             dot = __builtin_fma(B[o], A[o], dot);
         }
         if (ch.count == 1) return dot;
@@ -439,7 +553,7 @@ __global__ void k_fin_init(CgGeom G, ChunkArg ch, const double *__restrict__ acc
                            int32_t *__restrict__ nactive) {
     int64_t c = G.col0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (c >= G.col1) return;
-    double d = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.k, c, Rr, Rr);
+    double d = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.ld, c, Rr, Rr);
     double b = __builtin_sqrt(d);
     bn[c] = b;
     double at = rtol * b;  // max(atol=0, rtol*bnrm2)
@@ -447,7 +561,7 @@ __global__ void k_fin_init(CgGeom G, ChunkArg ch, const double *__restrict__ acc
     rho[c] = d;
     iters[c] = 0;
     int act = 1;
-    if (b == 0.0) act = 0;                 // cg returns b, info 0
+    if (b == 0.0) act = 0;                     // cg returns b, info 0
     else if (__builtin_sqrt(d) < at) act = 0;  // converged at loop top, iteration 0
     active[c] = act;
     if (act) atomicAdd(nactive, 1);
@@ -459,7 +573,7 @@ __global__ void k_fin_pq(CgGeom G, ChunkArg ch, const double *__restrict__ acc,
                          double *__restrict__ alpha) {
     int64_t c = G.col0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (c >= G.col1 || !active[c]) return;
-    double pq = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.k, c, P, Q);
+    double pq = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.ld, c, P, Q);
     alpha[c] = rho[c] / pq;
 }
 
@@ -471,7 +585,7 @@ __global__ void k_fin_rr(CgGeom G, ChunkArg ch, const double *__restrict__ acc,
                          int32_t *__restrict__ nactive) {
     int64_t c = G.col0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (c >= G.col1 || !active[c]) return;
-    double rr = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.k, c, Rr, Rr);
+    double rr = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.ld, c, Rr, Rr);
     rho_prev[c] = rho[c];
     rho[c] = rr;
     iters[c] = it + 1;
@@ -488,7 +602,7 @@ __global__ void k_x_init(CgGeom G, const double *__restrict__ Rr, const double *
     for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < G.n * ncol;
          idx += (int64_t)gridDim.x * blockDim.x) {
         int64_t i = idx / ncol, c = G.col0 + idx % ncol;
-        int64_t o = i * G.k + c;
+        int64_t o = i * G.ld + c;
         X[o] = (bn[c] == 0.0) ? Rr[o] : 0.0;
     }
 }
@@ -497,12 +611,12 @@ __global__ void k_x_init(CgGeom G, const double *__restrict__ Rr, const double *
 // r_eff[e] = 0 + pw_sum_c (Z_u,c - Z_v,c)^2 over columns [col0,col1),
 // Z = nan_to_num(X) (metrics.py:288,292-293); finalize: :296-297.
 __global__ void k_er_scores(const int32_t *__restrict__ rows, const int32_t *__restrict__ ix,
-                            const double *__restrict__ X, int64_t k, int64_t col0, int64_t col1,
+                            const double *__restrict__ X, int64_t ld, int64_t col0, int64_t col1,
                             int64_t e0, int64_t e1, int finalize, double *__restrict__ out) {
     for (int64_t e = e0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < e1;
          e += (int64_t)gridDim.x * blockDim.x) {
-        const double *zu = X + (int64_t)rows[e] * k + col0;
-        const double *zv = X + (int64_t)ix[e] * k + col0;
+        const double *zu = X + (int64_t)rows[e] * ld + col0;
+        const double *zv = X + (int64_t)ix[e] * ld + col0;
         double s = pw_sum<double>(col1 - col0, [&](int64_t c) {
             double a = zu[c], b = zv[c];
             if (a != a || __builtin_isinf(a)) a = 0.0;
@@ -599,7 +713,9 @@ int gs_er_prepare(gs_ctx *c, int64_t k, double reg, int64_t *m_out) {
                 g.indptr.as<int64_t>(), g.indices.as<int32_t>(), g.data.as<double>(), n, reg, lp,
                 er.li.as<int32_t>(), er.lv.as<double>());
         // state
-        size_t nk = sizeof(double) * (size_t)(n ? n : 1) * (size_t)k;
+        // row stride padded to 8 doubles: 64-B aligned rows, 16-B vector access
+        er.ld = (k + 7) & ~(int64_t)7;
+        size_t nk = sizeof(double) * (size_t)(n ? n : 1) * (size_t)er.ld;
         er.X.ensure(nk);
         er.Rr.ensure(nk);
         er.P0.ensure(nk);
@@ -632,8 +748,8 @@ int gs_er_project_rows(gs_ctx *c, int64_t e0, int64_t e1, const double *raw, int
         int64_t ncb = (er.k + 63) / 64;
         hipEvent_t t0 = prof_begin(c);
         k_project<<<grid_for(er.n * ncb * 64, 256, 65536), 256, 0, c->stream>>>(
-            er.bptr.as<int64_t>(), er.bcol.as<int64_t>(), er.bsgn.as<int8_t>(), er.bcur.as<int64_t>(),
-            er.n, er.k, e0, e1, draw, sqrt_k, er.Rr.as<double>());
+            er.bptr.as<int64_t>(), er.bcol.as<int64_t>(), er.bsgn.as<int8_t>(), er.n, er.k, er.ld,
+            e0, e1, draw, sqrt_k, er.Rr.as<double>());
         GS_HIP(hipGetLastError());
         prof_end(c, t0, "er_project", (double)bytes * 3.0);
         er.proj_next = e1;
@@ -653,22 +769,37 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         GS_HIP(hipSetDevice(c->device));
         const int64_t n = er.n, k = er.k;
         ChunkArg ch = to_arg(make_chunks(n, blas_threads));
-        CgGeom G{n, k, col0, col1};
+        // two columns per lane (16-B accesses) unless that leaves too few waves
+        const int64_t ncols = col1 - col0;
+        const int64_t waves2 = ((ncols + 127) / 128) * 32 * (int64_t)ch.count;
+        const int cpl = waves2 >= 4096 ? 2 : 1;
+        CgGeom G;
+        G.n = n;
+        G.k = k;
+        G.ld = er.ld;
+        G.col0 = col0;
+        G.col1 = col1;
+        G.ncb = (int32_t)((ncols + 64 * cpl - 1) / (64 * cpl));
+        G.npairs = G.ncb * ch.count;
         ColPtrs cp = col_ptrs(er);
         double *X = er.X.as<double>(), *Rr = er.Rr.as<double>(), *Q = er.Q.as<double>();
         double *P[2] = {er.P0.as<double>(), er.P1.as<double>()};
         double *acc = er.acc.as<double>();
-        const int64_t ncolb = (col1 - col0 + 63) / 64;
-        dim3 grid((unsigned)ncolb, 8, (unsigned)ch.count), block(256);
-        unsigned fgrid = grid_for(col1 - col0, 64);
-        const double bytes_pq = 32.0 * n * (col1 - col0), bytes_upd = 48.0 * n * (col1 - col0);
+        // 8 workgroups (32 residues) per (column block, chunk) pair, XCD-grouped
+        dim3 grid((unsigned)(((G.npairs + 7) / 8) * 64)), block(256);
+        unsigned fgrid = grid_for(ncols, 64);
+        const double bytes_pq = 32.0 * n * ncols, bytes_upd = 48.0 * n * ncols;
+        const int64_t *lp = er.lp.as<int64_t>();
+        const int32_t *li = er.li.as<int32_t>();
+        const double *lv = er.lv.as<double>();
         GS_HIP(hipMemsetAsync(cp.nactive, 0, sizeof(int32_t), c->stream));
         // ||b|| and rho_0 (r = b.copy())
-        k_dot_acc<<<grid, block, 0, c->stream>>>(G, ch, Rr, Rr, acc);
+        if (cpl == 2) k_dot_acc<2><<<grid, block, 0, c->stream>>>(G, ch, Rr, Rr, acc);
+        else k_dot_acc<1><<<grid, block, 0, c->stream>>>(G, ch, Rr, Rr, acc);
         k_fin_init<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Rr, rtol, cp.bn, cp.atol, cp.rho,
                                                  cp.active, cp.iters, cp.nactive);
         if (n)
-            k_x_init<<<grid_for(n * (col1 - col0), 256, 65536), 256, 0, c->stream>>>(G, Rr, cp.bn, X);
+            k_x_init<<<grid_for(n * ncols, 256, 65536), 256, 0, c->stream>>>(G, Rr, cp.bn, X);
         GS_HIP(hipGetLastError());
         int cur = 0;
         for (int32_t it = 0; it < maxiter; ++it) {
@@ -681,20 +812,24 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             }
             double *Pold = P[cur], *Pnew = P[cur ^ 1];
             hipEvent_t t0 = prof_begin(c);
-            if (it == 0)
-                k_cg_pq<true><<<grid, block, 0, c->stream>>>(G, ch, er.lp.as<int64_t>(),
-                                                             er.li.as<int32_t>(), er.lv.as<double>(),
-                                                             Rr, Pold, Pnew, Q, cp.rho, cp.rho_prev,
-                                                             cp.active, acc);
-            else
-                k_cg_pq<false><<<grid, block, 0, c->stream>>>(G, ch, er.lp.as<int64_t>(),
-                                                              er.li.as<int32_t>(), er.lv.as<double>(),
-                                                              Rr, Pold, Pnew, Q, cp.rho, cp.rho_prev,
-                                                              cp.active, acc);
-            prof_end(c, t0, "cg_pq", it == 0 ? bytes_pq - 8.0 * n * (col1 - col0) : bytes_pq);
+#define GS_PQ(F, C)                                                                           \
+    k_cg_pq<F, C><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Rr, Pold, Pnew, Q, cp.rho, \
+                                                cp.rho_prev, cp.active, acc)
+            if (it == 0) {
+                if (cpl == 2) GS_PQ(true, 2); else GS_PQ(true, 1);
+            } else {
+                if (cpl == 2) GS_PQ(false, 2); else GS_PQ(false, 1);
+            }
+#undef GS_PQ
+            prof_end(c, t0, "cg_pq", it == 0 ? bytes_pq - 8.0 * n * ncols : bytes_pq);
             k_fin_pq<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Pnew, Q, cp.rho, cp.active, cp.alpha);
             t0 = prof_begin(c);
-            k_cg_upd<<<grid, block, 0, c->stream>>>(G, ch, Pnew, Q, X, Rr, cp.alpha, cp.active, acc);
+            if (cpl == 2)
+                k_cg_upd<2><<<grid, block, 0, c->stream>>>(G, ch, Pnew, Q, X, Rr, cp.alpha, cp.active,
+                                                           acc);
+            else
+                k_cg_upd<1><<<grid, block, 0, c->stream>>>(G, ch, Pnew, Q, X, Rr, cp.alpha, cp.active,
+                                                           acc);
             prof_end(c, t0, "cg_upd", bytes_upd);
             k_fin_rr<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Rr, it, cp.rho, cp.rho_prev, cp.atol,
                                                   cp.active, cp.iters, cp.nactive);
@@ -723,7 +858,7 @@ int gs_er_scores(gs_ctx *c, int64_t col0, int64_t col1, int64_t e0, int64_t e1, 
         if (cnt) {
             hipEvent_t t0 = prof_begin(c);
             k_er_scores<<<grid_for(cnt, 64), 64, 0, c->stream>>>(
-                c->g.rows.as<int32_t>(), c->g.indices.as<int32_t>(), er.X.as<double>(), er.k, col0,
+                c->g.rows.as<int32_t>(), c->g.indices.as<int32_t>(), er.X.as<double>(), er.ld, col0,
                 col1, e0, e1, finalize, dout);
             GS_HIP(hipGetLastError());
             prof_end(c, t0, "er_scores", (16.0 * (col1 - col0) + 16.0) * cnt);
