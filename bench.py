@@ -1,22 +1,27 @@
 #!/usr/bin/env python3
 """Benchmark: scored edges/s of Jaccard + ApproxER (BASELINE.json metric).
 
-Workload at N=1 (configs[1]): the Roman-empire stand-in (roman_like: n=22,662,
-E=65,854 directed CSR entries, 32,927 undirected edges, k=2,674 JL columns,
-500 CG iterations per column -- every column hits maxiter on this chain-like
-graph, as on Roman-empire itself).  One step = Jaccard scores for all E
-edges + the full ApproxER pipeline (PCG64 normal stream -> Y = B R -> batched
-CG -> per-edge squared distances) with the CSR already resident in HBM.
+Default workload (configs[1], N=1): the Roman-empire stand-in (roman_like:
+n=22,662, E=65,854 directed CSR entries, 32,927 undirected edges, k=2,674 JL
+columns, 500 CG iterations per column -- every column hits maxiter on this
+chain-like graph, as on Roman-empire itself).  One step = Jaccard scores for
+all E edges + the full ApproxER pipeline (PCG64/ziggurat normal stream on the
+device -> Y = B R -> batched CG -> per-edge squared distances) with the CSR
+resident in HBM.
 
-N > 1 (one process per GPU, torchrun): the same problem strong-scaled --
-Jaccard by contiguous CSR edge ranges with an RCCL all-gather of the scores,
-ApproxER by blocks of JL columns cut along NumPy's pairwise-sum tree with an
-RCCL all-gather of the per-edge partial sums, combined in tree order (the
+N > 1 (torchrun, one process per GPU, RCCL over xGMI): the same problem
+strong-scaled through gsparse.distributed -- Jaccard by contiguous CSR edge
+ranges + all-gather of the scores, ApproxER by pairwise-tree blocks of JL
+columns + all-gather of the per-edge partial sums combined in tree order (the
 scores stay bit-identical to N=1).
+
+Other workloads (not the default line): --workload rmat (Jaccard-T on
+Graph500 R-MAT, configs[3]; --scale 22 by default), arxiv (configs[2]),
+backbone (configs[4]).
 
 Prints ONE JSON line (rank 0) with roofline (dominant kernel, HIP events on
 the library's stream) and cpu_baseline (the oracle's NumPy/SciPy restatement
-of the reference path, bounded sample, timed on this host).
+of the reference path, bounded sample, timed on this host, rank 0 at N=1).
 """
 
 from __future__ import annotations
@@ -40,12 +45,13 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(ei, n, k, sample_cols, threads):
+def cpu_baseline_roman(ei, n, sample_cols, threads):
     """The reference algorithm restated with identical NumPy/SciPy calls
     (oracle/gsparse_oracle.py), timed on a bounded sample of the same
     workload: full Jaccard (A@A + gather, metrics.py:43-62), full R stream and
-    Y = B @ R (metrics.py:272-275), CG on `sample_cols` of the k columns
-    (metrics.py:284-289), extrapolated by k/sample_cols."""
+    Y = B @ R (metrics.py:272-275), SciPy CG on `sample_cols` of the k columns
+    (metrics.py:284-289) extrapolated by k/sample_cols, and the diff^2 row sums
+    (metrics.py:292-293) extrapolated from 64 columns."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import scipy.sparse as sp
     import scipy.sparse.linalg as spla
@@ -87,8 +93,38 @@ def cpu_baseline(ei, n, k, sample_cols, threads):
         "sample": (f"full Jaccard ({t_jac:.3f}s) + full R/Y projection ({t_proj:.2f}s) + SciPy CG "
                    f"on {sample_cols}/{kk} columns x500 iters extrapolated ({t_cg:.1f}s) + "
                    f"diff^2 sum extrapolated ({t_fin:.2f}s); OpenBLAS threads={threads}"),
-        "seconds_extrapolated": total,
+        "seconds_extrapolated": round(total, 3),
     }
+
+
+def cpu_baseline_jaccard(ei, n, threads, max_edges=2_000_000):
+    """Reference-style SpGEMM Jaccard (metrics.py:43-62) on a row-prefix sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import scipy.sparse as sp
+    from threadpoolctl import threadpool_limits
+
+    import gsparse_oracle as O
+
+    ip, ix, d = O.canonical_csr(ei, n)
+    rows_cut = int(np.searchsorted(ip, min(max_edges, len(ix))))
+    sub = sp.csr_matrix((d[: ip[rows_cut]], ix[: ip[rows_cut]], ip[: rows_cut + 1]),
+                        shape=(rows_cut, n))
+    adj = sp.csr_matrix((d, ix, ip), shape=(n, n))
+    with threadpool_limits(limits=threads, user_api="blas"):
+        t0 = time.perf_counter()
+        ab = (sub > 0).astype(np.float64)
+        full = (adj > 0).astype(np.float64)
+        deg = np.asarray(full.sum(axis=1)).flatten()
+        inter = ab @ full
+        rows, cols = ab.nonzero()
+        ic = np.asarray(inter[rows, cols]).flatten()
+        uni = deg[rows] + deg[cols] - ic
+        _ = np.divide(ic, uni, out=np.zeros_like(ic), where=uni > 0)
+        t = time.perf_counter() - t0
+    return {"value": float(len(rows) / t), "unit": "scored edges/s", "cores": int(threads),
+            "kind": "port",
+            "sample": f"reference-style SpGEMM Jaccard on the first {len(rows)} CSR edges "
+                      f"({t:.2f}s); OpenBLAS threads={threads}"}
 
 
 def main():
@@ -96,6 +132,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="roman", choices=["roman", "rmat", "arxiv"])
+    ap.add_argument("--scale", type=int, default=22, help="R-MAT scale for --workload rmat")
     ap.add_argument("--blas-threads", type=int, default=8,
                     help="OpenBLAS ddot order to reproduce (reference run with this many threads)")
     ap.add_argument("--rng", default=os.environ.get("GSPARSE_ER_RNG", "device"),
@@ -106,62 +144,72 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; modulo the visible count so a 1-GPU box can rehearse N>1
+    local_rank = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        backend = os.environ.get("GSPARSE_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local_rank)
 
     from gsparse import graphs
     from gsparse._lib import Context
-    from gsparse.engine import Engine, er_split, jl_dim
+    from gsparse.distributed import Comm, sharded_approx_er, sharded_edge_scores, work_ranges
+    from gsparse.engine import Engine, jl_dim
 
-    ei = graphs.roman_like()
-    n = 22_662
+    t_gen = time.perf_counter()
+    if args.workload == "roman":
+        ei, n = graphs.roman_like(), 22_662
+        with_er = True
+        wl = "configs[1] Roman-empire Jaccard+ApproxER"
+    elif args.workload == "arxiv":
+        ei, n = graphs.citation_like(), 169_343
+        with_er = True
+        wl = "configs[2] ogbn-arxiv-size Jaccard+ApproxER"
+    else:
+        ei, n = graphs.rmat(args.scale, 8, seed=0), 1 << args.scale
+        with_er = False
+        wl = f"configs[3] RMAT-{args.scale} Jaccard-T"
+    t_gen = time.perf_counter() - t_gen
     E = ei.shape[1]
     ctx = Context(local_rank)
-    stream = torch.cuda.current_stream(dev)
-    ctx.set_stream(stream.cuda_stream)
     src = torch.from_numpy(np.ascontiguousarray(ei[0])).to(dev)
     dst = torch.from_numpy(np.ascontiguousarray(ei[1])).to(dev)
     ctx.set_graph_edge_index(n, src, dst)
+    del src, dst
     eng = Engine(ctx)
     nnz = eng.nnz
     k = jl_dim(n, 0.3)
-    # partitions
-    ebounds = [nnz * r // world for r in range(world + 1)]
-    e0, e1 = ebounds[rank], ebounds[rank + 1]
-    cb = er_split(k, world)
-    c0, c1 = cb[rank], cb[rank + 1]
-    emax = max(ebounds[r + 1] - ebounds[r] for r in range(world))
-    jac_local = torch.zeros(emax, dtype=torch.float64, device=dev)
-    er_local = torch.empty(nnz, dtype=torch.float64, device=dev)
+    comm = Comm(device=dev) if world > 1 else None
+    bounds = None
+    if world > 1 and args.workload == "rmat":
+        bounds = work_ranges(eng.indptr(), ctx.csr()[1], world)
+    jac_out = torch.empty(nnz, dtype=torch.float64, device=dev)
+    er_out = torch.empty(nnz, dtype=torch.float64, device=dev)
 
     def step():
-        eng.jaccard(e0, e1, out=jac_local[: e1 - e0])
-        rng = np.random.default_rng(42)
-        eng.er_prepare(k)
-        if args.rng == "device":
-            eng.er_project_device(rng, k)
-        else:
-            eng.er_project_host(rng, k)
-        eng.er_solve(c0, c1, 500, 1e-6, args.blas_threads)
-        eng.er_scores(c0, c1, finalize=(world == 1), out=er_local)
         if world > 1:
-            jac_all = [torch.empty_like(jac_local) for _ in range(world)]
-            dist.all_gather(jac_all, jac_local)
-            er_all = [torch.empty_like(er_local) for _ in range(world)]
-            dist.all_gather(er_all, er_local)
-            parts = er_all
-            while len(parts) > 1:  # NumPy pairwise tree order
-                parts = [parts[i] + parts[i + 1] for i in range(0, len(parts), 2)]
-            tot = 0.0 + parts[0]
-            tot = torch.nan_to_num(tot, nan=1e-10, posinf=1e-10, neginf=1e-10).clamp_min_(1e-10)
-            return torch.cat([jac_all[r][: ebounds[r + 1] - ebounds[r]] for r in range(world)]), tot
-        return jac_local[:nnz], er_local
+            jac = sharded_edge_scores(eng, comm, "jaccard", bounds=bounds)
+            er = sharded_approx_er(eng, comm, blas_threads=args.blas_threads,
+                                   rng_mode=args.rng) if with_er else None
+            return jac, er
+        eng.jaccard(0, nnz, out=jac_out)
+        if with_er:
+            rng = np.random.default_rng(42)
+            eng.er_prepare(k)
+            if args.rng == "device":
+                eng.er_project_device(rng, k)
+            else:
+                eng.er_project_host(rng, k)
+            eng.er_solve(0, k, 500, 1e-6, args.blas_threads)
+            eng.er_scores(0, k, True, out=er_out)
+        return jac_out, er_out
 
     for _ in range(args.warmup):
         step()
@@ -173,7 +221,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = step()
+        step()
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -182,27 +230,29 @@ def main():
     ctx.profile(False)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        if dist.get_backend() != "nccl":
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
-    value = E * args.steps / elapsed  # every step scores all E edges with both metrics
+    value = E * args.steps / elapsed  # every step scores all E edges (with both metrics)
 
-    # roofline: the dominant kernel by summed time
-    dom = max(prof.items(), key=lambda kv: kv[1]["ms"]) if prof else (None, None)
+    # roofline: the dominant kernel by summed time (HIP events on its stream)
     roofline = None
-    if dom[0]:
-        name, p = dom
+    if prof:
+        name, p = max(prof.items(), key=lambda kv: kv[1]["ms"])
         avg_ms = p["ms"] / p["launches"]
         bytes_per = p["bytes"] / p["launches"]
         achieved = bytes_per / (avg_ms * 1e-3) / 1e9
         roofline = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": None, "avg_launch_ms": round(avg_ms, 5),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "avg_launch_ms": round(avg_ms, 5),
                     "algorithmic_bytes_per_launch": bytes_per, "launches": p["launches"]}
     kernels = {k2: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k2, v in prof.items()}
 
     result = {
-        "metric": "scored edges/sec (Jaccard+ApproxER)",
+        "metric": "scored edges/sec (Jaccard+ApproxER)" if with_er else "scored edges/sec (Jaccard)",
         "value": round(value, 1),
         "unit": "scored edges/s",
         "n_gpus": world,
@@ -213,17 +263,22 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (roman_like stand-in; Roman-empire is not downloadable here)",
-        "config": {"workload": "configs[1] Roman-empire Jaccard+ApproxER", "n": n, "E": E,
-                   "jl_k": k, "cg_maxiter": 500, "blas_threads_order": args.blas_threads,
-                   "rng": args.rng, "parallelism": f"edges+jl-columns/{world}"},
+        "data": "synthetic (stand-in graph of the config's size; datasets are not downloadable here)",
+        "config": {"workload": wl, "n": n, "E": E, "jl_k": k if with_er else None,
+                   "cg_maxiter": 500 if with_er else None,
+                   "blas_threads_order": args.blas_threads, "rng": args.rng,
+                   "parallelism": f"edges+jl-columns/{world}" if world > 1 else "1 GPU",
+                   "graph_gen_s": round(t_gen, 2)},
         "roofline": roofline,
         "kernels": kernels,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # one BLAS thread: the fastest setting for this SciPy CG (n=22,662) on
         # the hosts measured (8 threads: 3.8x slower from ddot threading overhead)
-        result["cpu_baseline"] = cpu_baseline(ei, n, k, args.cpu_sample_cols, 1)
+        if args.workload == "roman":
+            result["cpu_baseline"] = cpu_baseline_roman(ei, n, args.cpu_sample_cols, 1)
+        elif args.workload == "rmat":
+            result["cpu_baseline"] = cpu_baseline_jaccard(ei, n, 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
