@@ -56,6 +56,7 @@ static Chunks make_chunks(int64_t n, int32_t threads) {
 struct ColPtrs {
     double *bn, *atol, *rho, *rho_prev, *alpha;
     int32_t *active, *iters;
+    int32_t *xstep;    // iteration whose (alpha, p) is still to be added to x
     int32_t *nactive;  // single counter
 };
 
@@ -70,7 +71,8 @@ static ColPtrs col_ptrs(ErState &er) {
     p.alpha = p.rho_prev + k;
     p.active = (int32_t *)(p.alpha + k);
     p.iters = p.active + k;
-    p.nactive = p.iters + k;
+    p.xstep = p.iters + k;
+    p.nactive = p.xstep + k;
     return p;
 }
 
@@ -310,6 +312,13 @@ struct Vec<2> {
     }
 };
 
+// Iteration t, kernel 1 (after beta_t is known):
+//   x += fl(alpha_{t-1} p_{t-1})   for columns whose previous update is pending
+//                                  (the x update of SciPy's iteration t-1, moved
+//                                  here so the second kernel never touches x or p)
+//   p_t = fl(fl(beta_t p_{t-1}) + r_t)  (own row stored; neighbours recomputed)
+//   q_t = L_reg p_t (per-row fold from 0.0, ascending column), kept only for the
+//         <32 leftover rows the ddot finish needs (qside); chains of dot(p_t, q_t).
 template <bool FIRST, int CPL>
 __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
                                                const int64_t *__restrict__ lp,
@@ -317,24 +326,31 @@ __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
                                                const double *__restrict__ lv,
                                                const double *__restrict__ R,
                                                const double *__restrict__ Pold,
-                                               double *__restrict__ Pnew, double *__restrict__ Q,
+                                               double *__restrict__ Pnew, double *__restrict__ X,
+                                               double *__restrict__ qside,
                                                const double *__restrict__ rho,
                                                const double *__restrict__ rho_prev,
+                                               const double *__restrict__ alpha,
                                                const int32_t *__restrict__ active,
+                                               const int32_t *__restrict__ xstep, int32_t it,
                                                double *__restrict__ acc) {
     const CgLane ln = cg_lane<CPL>(G);
     if (!ln.ok) return;
     const int64_t ld = G.ld, c = ln.c;
-    bool live[CPL];
-    double beta[CPL];
-    bool any = false;
+    bool live[CPL], xp[CPL];
+    double beta[CPL], al[CPL];
+    bool any_live = false, any_x = false;
 #pragma unroll
     for (int u = 0; u < CPL; ++u) {
-        live[u] = (c + u) < G.col1 && active[c + u];
+        const bool in = (c + u) < G.col1;
+        live[u] = in && active[c + u];
+        xp[u] = !FIRST && in && xstep[c + u] == it - 1;
         beta[u] = (!FIRST && live[u]) ? rho[c + u] / rho_prev[c + u] : 0.0;
-        any = any || live[u];
+        al[u] = xp[u] ? alpha[c + u] : 0.0;
+        any_live = any_live || live[u];
+        any_x = any_x || xp[u];
     }
-    if (!any) return;
+    if (!any_live && !any_x) return;
     const int64_t a = ch.a[ln.t], L = ch.len[ln.t];
     const int64_t n1 = L & ~(int64_t)15, n32 = n1 & ~(int64_t)31;
     double s[CPL];
@@ -342,13 +358,26 @@ __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
     for (int u = 0; u < CPL; ++u) s[u] = 0.0;
 
     auto row_pq = [&](int64_t row, double *pi, double *q) {
-        const int64_t e0 = lp[row], e1 = lp[row + 1];
-        bool found = false;
+        if (!FIRST && any_x) {
+            Vec<CPL> po, xv;
+            po.load(Pold + row * ld + c);
+            xv.load(X + row * ld + c);
+#pragma unroll
+            for (int u = 0; u < CPL; ++u)
+                if (xp[u]) {
+                    double t1 = al[u] * po.v[u];
+                    xv.v[u] = xv.v[u] + t1;
+                }
+            xv.store(X + row * ld + c);
+        }
 #pragma unroll
         for (int u = 0; u < CPL; ++u) {
             q[u] = 0.0;
             pi[u] = 0.0;
         }
+        if (!any_live) return;
+        const int64_t e0 = lp[row], e1 = lp[row + 1];
+        bool found = false;
         for (int64_t e = e0; e < e1; ++e) {
             const int32_t col = li[e];
             const double w = lv[e];
@@ -384,14 +413,17 @@ __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
                 }
             }
         }
-        Vec<CPL> po, qo;
+        Vec<CPL> pw;
 #pragma unroll
-        for (int u = 0; u < CPL; ++u) {
-            po.v[u] = pi[u];
-            qo.v[u] = q[u];
+        for (int u = 0; u < CPL; ++u) pw.v[u] = live[u] ? pi[u] : 0.0;
+        // columns that are not live keep their last p (the flush may need it)
+        if (CPL == 1 || (live[0] && live[CPL - 1])) {
+            pw.store(Pnew + row * ld + c);
+        } else {
+#pragma unroll
+            for (int u = 0; u < CPL; ++u)
+                if (live[u]) Pnew[row * ld + c + u] = pi[u];
         }
-        po.store(Pnew + row * ld + c);
-        qo.store(Q + row * ld + c);
     };
 
     for (int64_t row = a + ln.j; row < a + n32; row += 32) {
@@ -400,23 +432,36 @@ __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
 #pragma unroll
         for (int u = 0; u < CPL; ++u) s[u] = __builtin_fma(pi[u], q[u], s[u]);
     }
-    {  // leftover rows of the chunk (16-block + tail): computed, not accumulated
+    {  // leftover rows of the chunk (16-block + tail): q kept for the finish
         const int64_t row = a + n32 + ln.j;
         if (row < a + L) {
             double pi[CPL], q[CPL];
             row_pq(row, pi, q);
+            if (any_live) {
+                double *qs = qside + ((int64_t)ln.t * 32 + ln.j) * ld + c;
+#pragma unroll
+                for (int u = 0; u < CPL; ++u)
+                    if (live[u]) qs[u] = q[u];
+            }
         }
     }
+    if (any_live) {
 #pragma unroll
-    for (int u = 0; u < CPL; ++u)
-        if (c + u < G.col1) acc[((c + u - G.col0) * kMaxChunks + ln.t) * 32 + ln.j] = s[u];
+        for (int u = 0; u < CPL; ++u)
+            if (live[u]) acc[((c + u - G.col0) * kMaxChunks + ln.t) * 32 + ln.j] = s[u];
+    }
 }
 
+// Iteration t, kernel 2 (after alpha_t is known):
+//   q_t = L_reg p_t recomputed from the stored p_t (same fold, same bits),
+//   r_{t+1} = r_t - fl(alpha_t q_t); chains of dot(r_{t+1}, r_{t+1}).
 template <int CPL>
 __global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
+                                                const int64_t *__restrict__ lp,
+                                                const int32_t *__restrict__ li,
+                                                const double *__restrict__ lv,
                                                 const double *__restrict__ P,
-                                                const double *__restrict__ Q,
-                                                double *__restrict__ X, double *__restrict__ R,
+                                                double *__restrict__ R,
                                                 const double *__restrict__ alpha,
                                                 const int32_t *__restrict__ active,
                                                 double *__restrict__ acc) {
@@ -424,12 +469,13 @@ __global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
     if (!ln.ok) return;
     const int64_t ld = G.ld, c = ln.c;
     double al[CPL];
+    bool live[CPL];
     bool any = false;
 #pragma unroll
     for (int u = 0; u < CPL; ++u) {
-        bool live = (c + u) < G.col1 && active[c + u];
-        al[u] = live ? alpha[c + u] : 0.0;
-        any = any || live;
+        live[u] = (c + u) < G.col1 && active[c + u];
+        al[u] = live[u] ? alpha[c + u] : 0.0;
+        any = any || live[u];
     }
     if (!any) return;
     const int64_t a = ch.a[ln.t], L = ch.len[ln.t];
@@ -438,35 +484,32 @@ __global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
 #pragma unroll
     for (int u = 0; u < CPL; ++u) s[u] = 0.0;
     auto upd = [&](int64_t row, Vec<CPL> &rv) {
+        const int64_t e0 = lp[row], e1 = lp[row + 1];
+        double q[CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) q[u] = 0.0;
+        for (int64_t e = e0; e < e1; ++e) {
+            const int32_t col = li[e];
+            const double w = lv[e];
+            Vec<CPL> pv;
+            pv.load(P + col * ld + c);
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                double prod = w * pv.v[u];
+                q[u] = q[u] + prod;
+            }
+        }
         const int64_t o = row * ld + c;
-        Vec<CPL> xv, pv, qv;
-        xv.load(X + o);
-        pv.load(P + o);
-        qv.load(Q + o);
         rv.load(R + o);
 #pragma unroll
         for (int u = 0; u < CPL; ++u) {
-            double t1 = al[u] * pv.v[u];
-            xv.v[u] = xv.v[u] + t1;
-            double t2 = al[u] * qv.v[u];
-            rv.v[u] = rv.v[u] - t2;
+            double t2 = al[u] * q[u];
+            rv.v[u] = live[u] ? rv.v[u] - t2 : rv.v[u];
         }
-        xv.store(X + o);
         rv.store(R + o);
     };
     int64_t row = a + ln.j;
     const int64_t end = a + n32;
-    // two rows per trip: both rows' loads are in flight before either FMA
-    for (; row + 32 < end; row += 64) {
-        Vec<CPL> r0, r1;
-        upd(row, r0);
-        upd(row + 32, r1);
-#pragma unroll
-        for (int u = 0; u < CPL; ++u) {
-            s[u] = __builtin_fma(r0.v[u], r0.v[u], s[u]);
-            s[u] = __builtin_fma(r1.v[u], r1.v[u], s[u]);
-        }
-    }
     for (; row < end; row += 32) {
         Vec<CPL> r0;
         upd(row, r0);
@@ -482,7 +525,22 @@ __global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
     }
 #pragma unroll
     for (int u = 0; u < CPL; ++u)
-        if (c + u < G.col1) acc[((c + u - G.col0) * kMaxChunks + ln.t) * 32 + ln.j] = s[u];
+        if (live[u]) acc[((c + u - G.col0) * kMaxChunks + ln.t) * 32 + ln.j] = s[u];
+}
+
+// after the loop: the x update of the last executed iteration
+__global__ void k_x_flush(CgGeom G, const double *__restrict__ P, const double *__restrict__ alpha,
+                          const int32_t *__restrict__ xstep, int32_t it_last,
+                          double *__restrict__ X) {
+    int64_t ncol = G.col1 - G.col0;
+    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < G.n * ncol;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        int64_t i = idx / ncol, c = G.col0 + idx % ncol;
+        if (xstep[c] != it_last) continue;
+        int64_t o = i * G.ld + c;
+        double t1 = alpha[c] * P[o];
+        X[o] = X[o] + t1;
+    }
 }
 
 // plain dot accumulation (||b||^2 before the first iteration)
@@ -512,9 +570,11 @@ __global__ void __launch_bounds__(256) k_dot_acc(CgGeom G, ChunkArg ch,
 }
 
 // OpenBLAS ddot finish for one column: 32 chains -> value (see oracle_ddot).
-__device__ double ddot_finish(const double *__restrict__ acc_c, const ChunkArg &ch, int64_t ld,
+// Values of the (< 32) leftover rows of chunk t are A[row] and, when
+// Bside != nullptr, Bside[(t*32 + row - a - n32) * ld] (else B[row]).
+__device__ __noinline__ double ddot_finish(const double *__restrict__ acc_c, const ChunkArg &ch, int64_t ld,
                               int64_t c, const double *__restrict__ A,
-                              const double *__restrict__ B) {
+                              const double *__restrict__ B, const double *__restrict__ Bside) {
     double total = 0.0;
     for (int t = 0; t < ch.count; ++t) {
         const int64_t a = ch.a[t], L = ch.len[t];
@@ -527,8 +587,10 @@ __device__ double ddot_finish(const double *__restrict__ acc_c, const ChunkArg &
                 for (int l = 0; l < 4; ++l) b[4 * q + l] = a32[8 * q + l] + a32[8 * q + 4 + l];
             if (n1 > n32) {
                 for (int jj = 0; jj < 16; ++jj) {
-                    int64_t o = (a + n32 + jj) * ld + c;
-                    b[jj] = __builtin_fma(A[o], B[o], b[jj]);
+                    int64_t row = a + n32 + jj;
+                    double bv = Bside ? Bside[((int64_t)t * 32 + (row - a - n32)) * ld + c]
+                                      : B[row * ld + c];
+                    b[jj] = __builtin_fma(A[row * ld + c], bv, b[jj]);
                 }
             }
             double c4[4];
@@ -536,8 +598,8 @@ __device__ double ddot_finish(const double *__restrict__ acc_c, const ChunkArg &
             dot = (c4[0] + c4[2]) + (c4[1] + c4[3]);
         }
         for (int64_t i = a + n1; i < a + L; ++i) {
-            int64_t o = i * ld + c;
-            dot = __builtin_fma(B[o], A[o], dot);
+            double bv = Bside ? Bside[((int64_t)t * 32 + (i - a - n32)) * ld + c] : B[i * ld + c];
+            dot = __builtin_fma(bv, A[i * ld + c], dot);
         }
         if (ch.count == 1) return dot;
         total = total + dot;
@@ -550,16 +612,17 @@ __global__ void k_fin_init(CgGeom G, ChunkArg ch, const double *__restrict__ acc
                            const double *__restrict__ Rr, double rtol, double *__restrict__ bn,
                            double *__restrict__ atol, double *__restrict__ rho,
                            int32_t *__restrict__ active, int32_t *__restrict__ iters,
-                           int32_t *__restrict__ nactive) {
+                           int32_t *__restrict__ xstep, int32_t *__restrict__ nactive) {
     int64_t c = G.col0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (c >= G.col1) return;
-    double d = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.ld, c, Rr, Rr);
+    double d = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.ld, c, Rr, Rr, nullptr);
     double b = __builtin_sqrt(d);
     bn[c] = b;
     double at = rtol * b;  // max(atol=0, rtol*bnrm2)
     atol[c] = at;
     rho[c] = d;
     iters[c] = 0;
+    xstep[c] = -2;
     int act = 1;
     if (b == 0.0) act = 0;                     // cg returns b, info 0
     else if (__builtin_sqrt(d) < at) act = 0;  // converged at loop top, iteration 0
@@ -568,13 +631,14 @@ __global__ void k_fin_init(CgGeom G, ChunkArg ch, const double *__restrict__ acc
 }
 
 __global__ void k_fin_pq(CgGeom G, ChunkArg ch, const double *__restrict__ acc,
-                         const double *__restrict__ P, const double *__restrict__ Q,
+                         const double *__restrict__ P, const double *__restrict__ qside,
                          const double *__restrict__ rho, const int32_t *__restrict__ active,
-                         double *__restrict__ alpha) {
+                         int32_t it, double *__restrict__ alpha, int32_t *__restrict__ xstep) {
     int64_t c = G.col0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (c >= G.col1 || !active[c]) return;
-    double pq = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.ld, c, P, Q);
+    double pq = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.ld, c, P, nullptr, qside);
     alpha[c] = rho[c] / pq;
+    xstep[c] = it;  // x += alpha p is applied by the next k_cg_pq (or the flush)
 }
 
 // after the update of iteration `it`: rho_prev = rho; rho = r.r; loop-top test
@@ -585,7 +649,7 @@ __global__ void k_fin_rr(CgGeom G, ChunkArg ch, const double *__restrict__ acc,
                          int32_t *__restrict__ nactive) {
     int64_t c = G.col0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (c >= G.col1 || !active[c]) return;
-    double rr = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.ld, c, Rr, Rr);
+    double rr = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.ld, c, Rr, Rr, nullptr);
     rho_prev[c] = rho[c];
     rho[c] = rr;
     iters[c] = it + 1;
@@ -722,7 +786,7 @@ int gs_er_prepare(gs_ctx *c, int64_t k, double reg, int64_t *m_out) {
         er.P1.ensure(nk);
         er.Q.ensure(nk);
         GS_HIP(hipMemsetAsync(er.Rr.ptr, 0, nk, c->stream));
-        er.colstate.ensure(sizeof(double) * 5 * k + sizeof(int32_t) * (2 * k + 4));
+        er.colstate.ensure(sizeof(double) * 5 * k + sizeof(int32_t) * (3 * k + 4));
         GS_HIP(hipMemsetAsync(er.colstate.ptr, 0, er.colstate.bytes, c->stream));
         er.acc.ensure(sizeof(double) * (size_t)k * kMaxChunks * 32);
         er.iters.ensure(sizeof(int32_t) * k);
@@ -782,13 +846,18 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         G.ncb = (int32_t)((ncols + 64 * cpl - 1) / (64 * cpl));
         G.npairs = G.ncb * ch.count;
         ColPtrs cp = col_ptrs(er);
-        double *X = er.X.as<double>(), *Rr = er.Rr.as<double>(), *Q = er.Q.as<double>();
+        double *X = er.X.as<double>(), *Rr = er.Rr.as<double>();
+        // q of the < 32 leftover rows per chunk (the only q values the finish reads)
+        double *qside = (double *)er.Q.ensure(sizeof(double) * (size_t)ch.count * 32 * (size_t)er.ld);
         double *P[2] = {er.P0.as<double>(), er.P1.as<double>()};
         double *acc = er.acc.as<double>();
         // 8 workgroups (32 residues) per (column block, chunk) pair, XCD-grouped
         dim3 grid((unsigned)(((G.npairs + 7) / 8) * 64)), block(256);
         unsigned fgrid = grid_for(ncols, 64);
-        const double bytes_pq = 32.0 * n * ncols, bytes_upd = 48.0 * n * ncols;
+        // algorithmic bytes: pq reads x, p, r and writes x, p (first iteration: r in, p out);
+        // upd reads p, r and writes r
+        const double bytes_pq = 40.0 * n * ncols, bytes_pq0 = 16.0 * n * ncols,
+                     bytes_upd = 24.0 * n * ncols;
         const int64_t *lp = er.lp.as<int64_t>();
         const int32_t *li = er.li.as<int32_t>();
         const double *lv = er.lv.as<double>();
@@ -797,11 +866,12 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         if (cpl == 2) k_dot_acc<2><<<grid, block, 0, c->stream>>>(G, ch, Rr, Rr, acc);
         else k_dot_acc<1><<<grid, block, 0, c->stream>>>(G, ch, Rr, Rr, acc);
         k_fin_init<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Rr, rtol, cp.bn, cp.atol, cp.rho,
-                                                 cp.active, cp.iters, cp.nactive);
+                                                 cp.active, cp.iters, cp.xstep, cp.nactive);
         if (n)
             k_x_init<<<grid_for(n * ncols, 256, 65536), 256, 0, c->stream>>>(G, Rr, cp.bn, X);
         GS_HIP(hipGetLastError());
         int cur = 0;
+        int32_t it_last = -1;
         for (int32_t it = 0; it < maxiter; ++it) {
             if (it % 8 == 0) {
                 int32_t na = 0;
@@ -812,30 +882,38 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             }
             double *Pold = P[cur], *Pnew = P[cur ^ 1];
             hipEvent_t t0 = prof_begin(c);
-#define GS_PQ(F, C)                                                                           \
-    k_cg_pq<F, C><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Rr, Pold, Pnew, Q, cp.rho, \
-                                                cp.rho_prev, cp.active, acc)
+#define GS_PQ(F, C)                                                                             \
+    k_cg_pq<F, C><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Rr, Pold, Pnew, X, qside,    \
+                                                cp.rho, cp.rho_prev, cp.alpha, cp.active, cp.xstep, \
+                                                it, acc)
             if (it == 0) {
                 if (cpl == 2) GS_PQ(true, 2); else GS_PQ(true, 1);
             } else {
                 if (cpl == 2) GS_PQ(false, 2); else GS_PQ(false, 1);
             }
 #undef GS_PQ
-            prof_end(c, t0, "cg_pq", it == 0 ? bytes_pq - 8.0 * n * ncols : bytes_pq);
-            k_fin_pq<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Pnew, Q, cp.rho, cp.active, cp.alpha);
+            prof_end(c, t0, "cg_pq", it == 0 ? bytes_pq0 : bytes_pq);
+            k_fin_pq<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Pnew, qside, cp.rho, cp.active, it,
+                                                  cp.alpha, cp.xstep);
             t0 = prof_begin(c);
             if (cpl == 2)
-                k_cg_upd<2><<<grid, block, 0, c->stream>>>(G, ch, Pnew, Q, X, Rr, cp.alpha, cp.active,
-                                                           acc);
+                k_cg_upd<2><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Pnew, Rr, cp.alpha,
+                                                           cp.active, acc);
             else
-                k_cg_upd<1><<<grid, block, 0, c->stream>>>(G, ch, Pnew, Q, X, Rr, cp.alpha, cp.active,
-                                                           acc);
+                k_cg_upd<1><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Pnew, Rr, cp.alpha,
+                                                           cp.active, acc);
             prof_end(c, t0, "cg_upd", bytes_upd);
             k_fin_rr<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Rr, it, cp.rho, cp.rho_prev, cp.atol,
                                                   cp.active, cp.iters, cp.nactive);
             GS_HIP(hipGetLastError());
             cur ^= 1;
+            it_last = it;
         }
+        // the x update of the last executed iteration (P[cur] holds its p)
+        if (it_last >= 0 && n)
+            k_x_flush<<<grid_for(n * ncols, 256, 65536), 256, 0, c->stream>>>(G, P[cur], cp.alpha,
+                                                                              cp.xstep, it_last, X);
+        GS_HIP(hipGetLastError());
         er.pcur = cur;
         GS_HIP(hipMemcpyAsync(er.iters.ptr, cp.iters, sizeof(int32_t) * k, hipMemcpyDeviceToDevice,
                               c->stream));
