@@ -1,17 +1,23 @@
 #!/bin/bash
-# rocprofv3 summaries of the default bench workload (run on the GPU box).
+# rocprofv3 summaries of a bench workload (run on the GPU box).
 # Pass 1: kernel trace + stats; passes 2/3: HBM bytes (FETCH_SIZE, WRITE_SIZE)
 # in separate runs (MI355X_MICROARCH.md: TCC slots; FETCH_SIZE reads 1/2 of
-# the bytes of a wide coalesced stream on gfx950).
+# the bytes of a wide coalesced stream on gfx950); pass 4: L2 hit/miss.
+# usage: profile_bench.sh OUTDIR [bench args...]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/prof}
+shift || true
+ARGS="$*"
 mkdir -p "$OUT"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit $?
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $ARGS > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit $?
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err" || exit $?
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err" || exit $?
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/bench_write.json" 2> "$OUT/write.err" || exit $?
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > "$OUT/bench_write.json" 2> "$OUT/write.err" || exit $?
+timeout -k 10 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/l2" -o run -- \
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > "$OUT/bench_l2.json" 2> "$OUT/l2.err" || exit $?
+python3 tools/pmc_summary.py "$OUT/pmc_summary.json" "$OUT/fetch" "$OUT/write" "$OUT/l2" > "$OUT/pmc_summary.txt"
 echo "profile done"
