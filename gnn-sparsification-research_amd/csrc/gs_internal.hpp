@@ -170,4 +170,7 @@ void sort_pairs_u64_i64(gs_ctx *c, uint64_t *keys, int64_t *vals, int64_t n, int
 // Graph helpers used by the ER path (gs_graph.hip)
 void ensure_transpose(gs_ctx *c);
 
+// Whole-graph Jaccard of a symmetric graph (gs_jaccard.hip)
+void jaccard_symmetric(gs_ctx *c, double *out);
+
 }  // namespace gs

@@ -1,0 +1,346 @@
+// gs_jaccard.hip -- Jaccard (metrics.py:17-64) on symmetric graphs, whole edge set.
+//
+// For a symmetric graph |out(u) ∩ in(v)| = |N(u) ∩ N(v)| is symmetric in (u, v),
+// so each undirected pair is intersected ONCE, at its owner: the endpoint of
+// larger degree (ties: smaller id).  The owner row's neighbour set is put in a
+// hash table (LDS) or a bitmap (global, for rows too large for LDS) and the
+// other endpoint's -- shorter -- list is streamed and probed.  Work is
+// sum over pairs of min(d_u, d_v) probes instead of the d_u + d_v of a merge
+// (RMAT-22: 1.24e10 vs 2.9e11), and the same value is written to both CSR
+// entries (u,v) and (v,u) (rev(e) = tpos[e] on a symmetric graph).
+//
+// Rows are classed by degree:
+//   light (d <= 32): one thread per owned entry, sorted-list merge
+//   hash  (d <= 16384): tasks = (row, slice of its entries) sized to ~max(64K, 8 d)
+//                   probes; the workgroup builds the row's table in LDS
+//                   (capacity 2d..4d slots, 8 / 32 / 128 KiB classes), then each
+//                   wave takes one owned entry at a time, 64 list elements per step
+//   giant (d > 16384): same tasks against an n-bit bitmap of the row (global, L2)
+// Counts are integers and the value is the reference's single fp64 division,
+// so the output is bit-identical to the per-entry kernel in gs_scores.hip.
+#include "gs_internal.hpp"
+
+#include <vector>
+
+namespace gs {
+
+static constexpr int64_t kJacLight = 32;
+static constexpr int64_t kJacGiant = 16384;
+static constexpr int64_t kJacTaskMin = 65536;
+static constexpr int kJacClasses = 4;  // 3 LDS table sizes + bitmap
+
+__device__ __forceinline__ bool jac_owns(int64_t du, int64_t dv, int32_t u, int32_t v) {
+    return du > dv || (du == dv && u <= v);
+}
+
+__device__ __forceinline__ double jac_value(int64_t inter, int64_t du, int64_t dv) {
+    double uni = (double)du + (double)dv - (double)inter;
+    return uni > 0.0 ? (double)inter / uni : 0.0;
+}
+
+__host__ __device__ __forceinline__ int jac_class(int64_t d) {
+    if (d <= kJacLight) return -1;
+    if (d <= 1024) return 0;
+    if (d <= 4096) return 1;
+    if (d <= kJacGiant) return 2;
+    return 3;
+}
+
+// per row: class, task count (work = sum of d_v over owned entries)
+__global__ void k_jac_plan(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                           int64_t n, int8_t *__restrict__ cls, int32_t *__restrict__ ntask) {
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t a = ip[u], du = ip[u + 1] - a;
+        const int k = jac_class(du);
+        int64_t nt = 0;
+        if (k >= 0) {
+            int64_t w = 0;
+            for (int64_t e = a; e < a + du; ++e) {
+                const int32_t v = ix[e];
+                const int64_t dv = ip[v + 1] - ip[v];
+                if (jac_owns(du, dv, (int32_t)u, v)) w += dv;
+            }
+            const int64_t t = du * 8 > kJacTaskMin ? du * 8 : kJacTaskMin;
+            nt = w ? (w + t - 1) / t : 0;
+            if (nt > du) nt = du;
+        }
+        cls[u] = (int8_t)k;
+        ntask[u] = (int32_t)nt;
+    }
+}
+
+__global__ void k_jac_mask(const int8_t *__restrict__ cls, const int32_t *__restrict__ ntask,
+                           int64_t n, int k, int64_t *__restrict__ cnt, int64_t *__restrict__ gflag) {
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        const bool in = cls[u] == k;
+        cnt[u] = in ? ntask[u] : 0;
+        if (gflag) gflag[u] = (in && ntask[u] > 0) ? 1 : 0;
+    }
+}
+
+// tasks of class k in row order; giant rows also get their bitmap slot
+__global__ void k_jac_emit(const int8_t *__restrict__ cls, const int32_t *__restrict__ ntask,
+                           const int64_t *__restrict__ off, const int64_t *__restrict__ goff,
+                           int64_t n, int k, int32_t *__restrict__ trow, int32_t *__restrict__ ti,
+                           int32_t *__restrict__ tslot, int32_t *__restrict__ grow) {
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        if (cls[u] != k) continue;
+        const int32_t nt = ntask[u];
+        if (!nt) continue;
+        const int64_t o = off[u];
+        const int32_t g = goff ? (int32_t)goff[u] : 0;
+        if (goff) grow[g] = (int32_t)u;
+        for (int32_t i = 0; i < nt; ++i) {
+            trow[o + i] = (int32_t)u;
+            ti[o + i] = i;
+            if (tslot) tslot[o + i] = g;
+        }
+    }
+}
+
+// light rows: one thread per owned entry, merge of two <= 32-long sorted lists
+__global__ void __launch_bounds__(256) k_jac_light(const int64_t *__restrict__ ip,
+                                                   const int32_t *__restrict__ ix,
+                                                   const int32_t *__restrict__ rows,
+                                                   const int64_t *__restrict__ rev, int64_t nnz,
+                                                   double *__restrict__ out) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t u = rows[e];
+        const int64_t a = ip[u], du = ip[u + 1] - a;
+        if (du > kJacLight) continue;
+        const int32_t v = ix[e];
+        const int64_t b = ip[v], dv = ip[v + 1] - b;
+        if (!jac_owns(du, dv, u, v)) continue;
+        int64_t i = 0, j = 0, cnt = 0;
+        while (i < du && j < dv) {
+            const int32_t x = ix[a + i], y = ix[b + j];
+            cnt += (x == y);
+            i += (x <= y);
+            j += (y <= x);
+        }
+        const double val = jac_value(cnt, du, dv);
+        out[e] = val;
+        out[rev[e]] = val;
+    }
+}
+
+__device__ __forceinline__ uint32_t jac_hash(int32_t x) { return (uint32_t)x * 2654435761u; }
+
+// Probe phase shared by the LDS-table and bitmap kernels: the workgroup's
+// waves take the owned entries of [lo, hi) of row u in turn.
+template <class Probe>
+__device__ __forceinline__ void jac_probe_entries(const int64_t *__restrict__ ip,
+                                                  const int32_t *__restrict__ ix,
+                                                  const int64_t *__restrict__ rev, int32_t u,
+                                                  int64_t du, int64_t lo, int64_t hi,
+                                                  double *__restrict__ out, Probe probe) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int64_t e = lo + wave; e < hi; e += nw) {
+        const int32_t v = ix[e];
+        const int64_t b = ip[v], dv = ip[v + 1] - b;
+        if (!jac_owns(du, dv, u, v)) continue;
+        int64_t cnt = 0;
+        for (int64_t j0 = 0; j0 < dv; j0 += 64) {
+            const int64_t j = j0 + lane;
+            const bool hit = j < dv && probe(ix[b + j]);
+            cnt += __popcll(__ballot(hit));
+        }
+        if (lane == 0) {
+            const double val = jac_value(cnt, du, dv);
+            out[e] = val;
+            out[rev[e]] = val;
+        }
+    }
+}
+
+__device__ __forceinline__ void jac_task_range(const int64_t *__restrict__ ip,
+                                               const int32_t *__restrict__ ntask, int32_t u,
+                                               int32_t i, int64_t &a, int64_t &du, int64_t &lo,
+                                               int64_t &hi) {
+    a = ip[u];
+    du = ip[u + 1] - a;
+    const int64_t nt = ntask[u];
+    lo = a + du * i / nt;
+    hi = a + du * (i + 1) / nt;
+}
+
+// one task per workgroup; table of C int32 slots in LDS (empty = -1)
+template <int C>
+__global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ ip,
+                                                   const int32_t *__restrict__ ix,
+                                                   const int64_t *__restrict__ rev,
+                                                   const int32_t *__restrict__ ntask,
+                                                   const int32_t *__restrict__ trow,
+                                                   const int32_t *__restrict__ ti,
+                                                   double *__restrict__ out) {
+    __shared__ int32_t tab[C];
+    const int32_t u = trow[blockIdx.x];
+    int64_t a, du, lo, hi;
+    jac_task_range(ip, ntask, u, ti[blockIdx.x], a, du, lo, hi);
+    for (int s = threadIdx.x; s < C; s += blockDim.x) tab[s] = -1;
+    __syncthreads();
+    constexpr uint32_t shift = 32 - __builtin_ctz(C);
+    for (int64_t e = a + threadIdx.x; e < a + du; e += blockDim.x) {
+        const int32_t x = ix[e];
+        uint32_t h = jac_hash(x) >> shift;
+        while (true) {
+            const int32_t prev = atomicCAS(&tab[h], -1, x);
+            if (prev == -1 || prev == x) break;
+            h = (h + 1) & (C - 1);
+        }
+    }
+    __syncthreads();
+    jac_probe_entries(ip, ix, rev, u, du, lo, hi, out, [&](int32_t x) {
+        uint32_t h = jac_hash(x) >> shift;
+        while (true) {
+            const int32_t k = tab[h];
+            if (k == x) return true;
+            if (k == -1) return false;
+            h = (h + 1) & (C - 1);
+        }
+    });
+}
+
+__global__ void k_jac_bitmap_build(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                                   const int32_t *__restrict__ grow, int32_t g0, int64_t words,
+                                   uint32_t *__restrict__ bm) {
+    const int32_t u = grow[g0 + blockIdx.y];
+    uint32_t *m = bm + (int64_t)blockIdx.y * words;
+    for (int64_t e = ip[u] + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ip[u + 1];
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t x = ix[e];
+        atomicOr(&m[x >> 5], 1u << (x & 31));
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_jac_bitmap(const int64_t *__restrict__ ip,
+                                                     const int32_t *__restrict__ ix,
+                                                     const int64_t *__restrict__ rev,
+                                                     const int32_t *__restrict__ ntask,
+                                                     const int32_t *__restrict__ trow,
+                                                     const int32_t *__restrict__ ti,
+                                                     const int32_t *__restrict__ tslot,
+                                                     int64_t t0, int32_t g0, int64_t words,
+                                                     const uint32_t *__restrict__ bm,
+                                                     double *__restrict__ out) {
+    const int64_t t = t0 + blockIdx.x;
+    const int32_t u = trow[t];
+    int64_t a, du, lo, hi;
+    jac_task_range(ip, ntask, u, ti[t], a, du, lo, hi);
+    const uint32_t *m = bm + (int64_t)(tslot[t] - g0) * words;
+    jac_probe_entries(ip, ix, rev, u, du, lo, hi, out,
+                      [&](int32_t x) { return ((m[x >> 5] >> (x & 31)) & 1u) != 0; });
+}
+
+// B_J for a symmetric graph: 8 * sum_u d_u^2 + 12 * nnz
+__global__ void k_jac_bytes(const int64_t *__restrict__ ip, int64_t n,
+                            unsigned long long *__restrict__ acc) {
+    unsigned long long s = 0;
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long d = (unsigned long long)(ip[u + 1] - ip[u]);
+        s += d * d;
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(acc, s);
+}
+
+// Whole-graph Jaccard of a symmetric graph into device out[nnz].
+void jaccard_symmetric(gs_ctx *c, double *out) {
+    Graph &g = c->g;
+    const int64_t n = g.n, nnz = g.nnz;
+    if (!nnz) return;
+    hipStream_t st = c->stream;
+    const int64_t *ip = g.indptr.as<int64_t>();
+    const int32_t *ix = g.indices.as<int32_t>();
+    const int64_t *rev = g.tpos.as<int64_t>();
+    double algo = 0.0;
+    if (c->profiling) {
+        auto *acc = (unsigned long long *)c->buf("jac_bytes").ensure(8);
+        GS_HIP(hipMemsetAsync(acc, 0, 8, st));
+        k_jac_bytes<<<grid_for(n, 256, 4096), 256, 0, st>>>(ip, n, acc);
+        unsigned long long s = 0;
+        GS_HIP(hipMemcpyAsync(&s, acc, 8, hipMemcpyDeviceToHost, st));
+        GS_HIP(hipStreamSynchronize(st));
+        algo = 8.0 * (double)s + 12.0 * (double)nnz;
+    }
+    hipEvent_t t0 = prof_begin(c);
+    auto *cls = (int8_t *)c->buf("jac_cls").ensure(n);
+    auto *ntask = (int32_t *)c->buf("jac_ntask").ensure(sizeof(int32_t) * n);
+    auto *cnt = (int64_t *)c->buf("jac_cnt").ensure(sizeof(int64_t) * (n + 1));
+    auto *off = (int64_t *)c->buf("jac_off").ensure(sizeof(int64_t) * (n + 1));
+    auto *gfl = (int64_t *)c->buf("jac_gflag").ensure(sizeof(int64_t) * (n + 1));
+    auto *goff = (int64_t *)c->buf("jac_goff").ensure(sizeof(int64_t) * (n + 1));
+    k_jac_plan<<<grid_for(n, 256, 16384), 256, 0, st>>>(ip, ix, n, cls, ntask);
+    k_jac_light<<<grid_for(nnz, 256, 65536), 256, 0, st>>>(ip, ix, g.rows.as<int32_t>(), rev, nnz,
+                                                           out);
+    GS_HIP(hipGetLastError());
+    for (int k = 0; k < kJacClasses; ++k) {
+        const bool giant = k == 3;
+        GS_HIP(hipMemsetAsync(cnt + n, 0, sizeof(int64_t), st));
+        GS_HIP(hipMemsetAsync(gfl + n, 0, sizeof(int64_t), st));
+        k_jac_mask<<<grid_for(n, 256, 16384), 256, 0, st>>>(cls, ntask, n, k, cnt,
+                                                            giant ? gfl : nullptr);
+        exclusive_scan_i64(c, cnt, off, n + 1);
+        if (giant) exclusive_scan_i64(c, gfl, goff, n + 1);
+        int64_t tot[2] = {0, 0};
+        GS_HIP(hipMemcpyAsync(&tot[0], off + n, 8, hipMemcpyDeviceToHost, st));
+        if (giant) GS_HIP(hipMemcpyAsync(&tot[1], goff + n, 8, hipMemcpyDeviceToHost, st));
+        GS_HIP(hipStreamSynchronize(st));
+        const int64_t ntot = tot[0], ngiant = tot[1];
+        if (!ntot) continue;
+        auto *trow = (int32_t *)c->buf("jac_trow").ensure(sizeof(int32_t) * ntot);
+        auto *ti = (int32_t *)c->buf("jac_ti").ensure(sizeof(int32_t) * ntot);
+        int32_t *tslot = giant ? (int32_t *)c->buf("jac_tslot").ensure(sizeof(int32_t) * ntot)
+                               : nullptr;
+        int32_t *grow = giant ? (int32_t *)c->buf("jac_grow").ensure(sizeof(int32_t) * ngiant)
+                              : nullptr;
+        k_jac_emit<<<grid_for(n, 256, 16384), 256, 0, st>>>(cls, ntask, off, giant ? goff : nullptr,
+                                                            n, k, trow, ti, tslot, grow);
+        GS_HIP(hipGetLastError());
+        GS_CHECK(ntot <= INT32_MAX, GS_EUNSUPPORTED, "too many Jaccard tasks (%lld)", (long long)ntot);
+        const unsigned nb = (unsigned)ntot;
+        if (k == 0) {
+            k_jac_hash<2048><<<nb, 256, 0, st>>>(ip, ix, rev, ntask, trow, ti, out);
+        } else if (k == 1) {
+            k_jac_hash<8192><<<nb, 512, 0, st>>>(ip, ix, rev, ntask, trow, ti, out);
+        } else if (k == 2) {
+            k_jac_hash<32768><<<nb, 1024, 0, st>>>(ip, ix, rev, ntask, trow, ti, out);
+        } else {
+            // bitmaps in batches of rows (<= 1 GiB of bits at a time)
+            const int64_t words = (n + 31) / 32;
+            int64_t per = ((int64_t)1 << 30) / (4 * words);
+            if (per < 1) per = 1;
+            std::vector<int32_t> hrow(ngiant);
+            GS_HIP(hipMemcpyAsync(hrow.data(), grow, sizeof(int32_t) * ngiant,
+                                  hipMemcpyDeviceToHost, st));
+            GS_HIP(hipStreamSynchronize(st));
+            for (int64_t g0 = 0; g0 < ngiant; g0 += per) {
+                const int64_t g1 = g0 + per < ngiant ? g0 + per : ngiant;
+                // task range of rows hrow[g0 .. g1): tasks are in row order
+                int64_t tb[2];
+                GS_HIP(hipMemcpyAsync(&tb[0], off + hrow[g0], 8, hipMemcpyDeviceToHost, st));
+                if (g1 < ngiant)
+                    GS_HIP(hipMemcpyAsync(&tb[1], off + hrow[g1], 8, hipMemcpyDeviceToHost, st));
+                GS_HIP(hipStreamSynchronize(st));
+                if (g1 >= ngiant) tb[1] = ntot;
+                auto *bm = (uint32_t *)c->buf("jac_bitmap").ensure(sizeof(uint32_t) * words * (g1 - g0));
+                GS_HIP(hipMemsetAsync(bm, 0, sizeof(uint32_t) * words * (g1 - g0), st));
+                k_jac_bitmap_build<<<dim3(64, (unsigned)(g1 - g0)), 256, 0, st>>>(
+                    ip, ix, grow, (int32_t)g0, words, bm);
+                if (tb[1] > tb[0])
+                    k_jac_bitmap<<<(unsigned)(tb[1] - tb[0]), 1024, 0, st>>>(
+                        ip, ix, rev, ntask, trow, ti, tslot, tb[0], (int32_t)g0, words, bm, out);
+                GS_HIP(hipGetLastError());
+            }
+        }
+        GS_HIP(hipGetLastError());
+    }
+    prof_end(c, t0, "jaccard", algo);
+}
+
+}  // namespace gs

@@ -14,6 +14,9 @@
 #include "gs_internal.hpp"
 #include "gs_pairwise.hpp"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace gs {
 
 // first index in b[lo..hi) with b[i] >= x (b sorted ascending)
@@ -234,7 +237,11 @@ int gs_jaccard(gs_ctx *c, int64_t e0, int64_t e1, double *out, int loc) {
         Graph &g = c->g;
         int64_t cnt = e1 - e0;
         double *dout = (double *)out_device(c, c->outbuf, out, sizeof(double) * cnt, loc);
-        if (cnt) {
+        const char *mode = getenv("GSPARSE_JACCARD");
+        const bool merge_only = mode && strcmp(mode, "merge") == 0;
+        if (cnt && g.symmetric && e0 == 0 && e1 == g.nnz && !merge_only) {
+            jaccard_symmetric(c, dout);  // owner-side hash/bitmap probing, both entries written
+        } else if (cnt) {
             const int64_t *tp = g.symmetric ? g.indptr.as<int64_t>() : g.tptr.as<int64_t>();
             const int32_t *ti = g.symmetric ? g.indices.as<int32_t>() : g.tidx.as<int32_t>();
             hipEvent_t t0 = prof_begin(c);

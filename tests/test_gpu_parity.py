@@ -167,6 +167,40 @@ def test_rmat14_vs_oracle(gs, rmat14):
     assert bits_equal(np.concatenate(parts), sp_.compute_scores("jaccard"))
 
 
+def _hub_graph():
+    """RMAT-14 plus hubs in every Jaccard row class of gs_jaccard.hip (LDS tables
+    of 2K / 8K / 32K slots and the > 16384 bitmap rows), hub-hub edges and
+    self-loops; symmetrised."""
+    from gsparse import graphs
+
+    n = 60000
+    parts = [graphs.rmat(14, 8, seed=11)]
+    for hub, lo, cnt in [(1, 100, 20000), (2, 50, 10000), (3, 7, 3000), (4, 1000, 800),
+                         (5, 30000, 17000)]:
+        leaves = np.arange(lo, lo + cnt, dtype=np.int64)
+        parts.append(np.stack([np.full(cnt, hub), leaves]))
+    parts.append(np.array([[1, 2, 3, 1, 5], [2, 3, 4, 5, 2]], dtype=np.int64))
+    loops = np.arange(0, 12, dtype=np.int64)
+    parts.append(np.stack([loops, loops]))
+    ei = np.concatenate(parts, axis=1)
+    ei = np.concatenate([ei, ei[::-1]], axis=1)
+    return ei, n
+
+
+def test_jaccard_owner_hash_classes_vs_oracle(gs, monkeypatch):
+    ei, n = _hub_graph()
+    ip, ix, _ = O.canonical_csr(ei, n)
+    assert np.diff(ip).max() > 16384
+    ref = O.jaccard(ip, ix)
+    data = gs.Data(edge_index=torch.from_numpy(ei), num_nodes=n)
+    sp_ = gs.GraphSparsifier(data, "cpu")
+    e = sp_._engine
+    assert e.symmetric
+    assert bits_equal(e.jaccard(), ref)
+    monkeypatch.setenv("GSPARSE_JACCARD", "merge")
+    assert bits_equal(e.jaccard(), ref)
+
+
 def test_backbone_rmat12_vs_oracle(gs):
     from gsparse import graphs
 
