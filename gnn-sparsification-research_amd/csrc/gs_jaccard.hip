@@ -28,6 +28,9 @@ static constexpr int64_t kJacLight = 32;
 static constexpr int64_t kJacGiant = 16384;
 static constexpr int64_t kJacTaskMin = 65536;
 static constexpr int kJacClasses = 4;  // 3 LDS table sizes + bitmap
+static constexpr int kJacUnroll = 4;   // list elements per lane in flight
+static constexpr int kJacMaxEnt = 1024;  // entries per task (LDS staging)
+static constexpr int64_t kJacSmall = 16;  // d_v <= this: 16-lane groups
 
 __device__ __forceinline__ bool jac_owns(int64_t du, int64_t dv, int32_t u, int32_t v) {
     return du > dv || (du == dv && u <= v);
@@ -46,27 +49,45 @@ __host__ __device__ __forceinline__ int jac_class(int64_t d) {
     return 3;
 }
 
-// per row: class, task count (work = sum of d_v over owned entries)
-__global__ void k_jac_plan(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
-                           int64_t n, int8_t *__restrict__ cls, int32_t *__restrict__ ntask) {
-    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
-         u += (int64_t)gridDim.x * blockDim.x) {
+// probes per task: enough to amortise clearing the C-slot table and the d_u inserts
+__host__ __device__ __forceinline__ int64_t jac_task_probes(int k, int64_t du) {
+    const int64_t tab = k == 0 ? 2048 : k == 1 ? 8192 : k == 2 ? 32768 : 0;
+    int64_t t = 16 * tab > 8 * du ? 16 * tab : 8 * du;
+    return t > kJacTaskMin ? t : kJacTaskMin;
+}
+
+// per row (one wave each): class, task count (work = sum of d_v over owned entries)
+__global__ void __launch_bounds__(256) k_jac_plan(const int64_t *__restrict__ ip,
+                                                  const int32_t *__restrict__ ix, int64_t n,
+                                                  int8_t *__restrict__ cls,
+                                                  int32_t *__restrict__ ntask) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t u = w0; u < n; u += nw) {
         const int64_t a = ip[u], du = ip[u + 1] - a;
         const int k = jac_class(du);
-        int64_t nt = 0;
+        int64_t w = 0;
         if (k >= 0) {
-            int64_t w = 0;
-            for (int64_t e = a; e < a + du; ++e) {
+            for (int64_t e = a + lane; e < a + du; e += 64) {
                 const int32_t v = ix[e];
                 const int64_t dv = ip[v + 1] - ip[v];
                 if (jac_owns(du, dv, (int32_t)u, v)) w += dv;
             }
-            const int64_t t = du * 8 > kJacTaskMin ? du * 8 : kJacTaskMin;
-            nt = w ? (w + t - 1) / t : 0;
-            if (nt > du) nt = du;
+            for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o);
         }
-        cls[u] = (int8_t)k;
-        ntask[u] = (int32_t)nt;
+        if (lane == 0) {
+            int64_t nt = 0;
+            if (k >= 0 && w) {
+                const int64_t t = jac_task_probes(k, du);
+                nt = (w + t - 1) / t;
+                const int64_t ne = (du + kJacMaxEnt - 1) / kJacMaxEnt;
+                if (nt < ne) nt = ne;
+                if (nt > du) nt = du;
+            }
+            cls[u] = (int8_t)k;
+            ntask[u] = (int32_t)nt;
+        }
     }
 }
 
@@ -130,26 +151,74 @@ __global__ void __launch_bounds__(256) k_jac_light(const int64_t *__restrict__ i
 
 __device__ __forceinline__ uint32_t jac_hash(int32_t x) { return (uint32_t)x * 2654435761u; }
 
-// Probe phase shared by the LDS-table and bitmap kernels: the workgroup's
-// waves take the owned entries of [lo, hi) of row u in turn.
-template <class Probe>
-__device__ __forceinline__ void jac_probe_entries(const int64_t *__restrict__ ip,
-                                                  const int32_t *__restrict__ ix,
-                                                  const int64_t *__restrict__ rev, int32_t u,
-                                                  int64_t du, int64_t lo, int64_t hi,
-                                                  double *__restrict__ out, Probe probe) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int64_t e = lo + wave; e < hi; e += nw) {
+// Owned entries of a task, staged in LDS: (list base, length, entry offset).
+// Entries with d_v > kJacSmall fill the front and are taken one per wave;
+// short ones fill the back and are taken four per wave (16-lane groups).
+struct JacStage {
+    int64_t b[kJacMaxEnt];
+    int32_t dv[kJacMaxEnt];
+    int16_t off[kJacMaxEnt];
+    int nbig, nsmall;
+};
+
+__device__ __forceinline__ void jac_stage(const int64_t *__restrict__ ip,
+                                          const int32_t *__restrict__ ix, int32_t u, int64_t du,
+                                          int64_t lo, int64_t hi, JacStage &st) {
+    for (int64_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
         const int32_t v = ix[e];
         const int64_t b = ip[v], dv = ip[v + 1] - b;
         if (!jac_owns(du, dv, u, v)) continue;
+        const int k = dv > kJacSmall ? atomicAdd(&st.nbig, 1)
+                                     : kJacMaxEnt - 1 - atomicAdd(&st.nsmall, 1);
+        st.b[k] = b;
+        st.dv[k] = (int32_t)dv;
+        st.off[k] = (int16_t)(e - lo);
+    }
+}
+
+// Probe phase shared by the LDS-table and bitmap kernels (after jac_stage and
+// a barrier).  The d_u of the owner and each entry's d_v give the union.
+template <class Probe>
+__device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
+                                                 const int64_t *__restrict__ rev, int64_t du,
+                                                 int64_t lo, const JacStage &st,
+                                                 double *__restrict__ out, Probe probe) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int k = wave; k < st.nbig; k += nw) {
+        const int64_t b = st.b[k], dv = st.dv[k];
         int64_t cnt = 0;
-        for (int64_t j0 = 0; j0 < dv; j0 += 64) {
-            const int64_t j = j0 + lane;
-            const bool hit = j < dv && probe(ix[b + j]);
-            cnt += __popcll(__ballot(hit));
+        for (int64_t j0 = 0; j0 < dv; j0 += 64 * kJacUnroll) {
+            int32_t xs[kJacUnroll];  // all loads in flight before the first probe
+#pragma unroll
+            for (int t = 0; t < kJacUnroll; ++t) {
+                const int64_t j = j0 + t * 64 + lane;
+                xs[t] = j < dv ? ix[b + j] : -1;
+            }
+#pragma unroll
+            for (int t = 0; t < kJacUnroll; ++t) {
+                const bool hit = xs[t] >= 0 && probe(xs[t]);
+                cnt += __popcll(__ballot(hit));
+            }
         }
         if (lane == 0) {
+            const int64_t e = lo + st.off[k];
+            const double val = jac_value(cnt, du, dv);
+            out[e] = val;
+            out[rev[e]] = val;
+        }
+    }
+    const int grp = lane >> 4, gl = lane & 15;
+    const uint64_t gmask = 0xFFFFull << (16 * grp);
+    for (int r = wave * 4; r < st.nsmall; r += nw * 4) {
+        const int idx = r + grp;
+        const bool ok = idx < st.nsmall;
+        const int k = kJacMaxEnt - 1 - (ok ? idx : 0);
+        const int64_t dv = ok ? st.dv[k] : 0;
+        const int32_t x = gl < dv ? ix[st.b[k] + gl] : -1;
+        const bool hit = x >= 0 && probe(x);
+        const int64_t cnt = __popcll(__ballot(hit) & gmask);
+        if (ok && gl == 0) {
+            const int64_t e = lo + st.off[k];
             const double val = jac_value(cnt, du, dv);
             out[e] = val;
             out[rev[e]] = val;
@@ -177,30 +246,41 @@ __global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ i
                                                    const int32_t *__restrict__ trow,
                                                    const int32_t *__restrict__ ti,
                                                    double *__restrict__ out) {
-    __shared__ int32_t tab[C];
+    // 4-slot buckets (one 16-B LDS read per probe step); a bucket fills from
+    // slot 0 up, so a bucket with a free slot 3 ends an unsuccessful search
+    __shared__ int4 tab[C / 4];
+    __shared__ JacStage st;
     const int32_t u = trow[blockIdx.x];
     int64_t a, du, lo, hi;
     jac_task_range(ip, ntask, u, ti[blockIdx.x], a, du, lo, hi);
-    for (int s = threadIdx.x; s < C; s += blockDim.x) tab[s] = -1;
+    if (threadIdx.x == 0) st.nbig = st.nsmall = 0;
+    for (int s = threadIdx.x; s < C / 4; s += blockDim.x) tab[s] = make_int4(-1, -1, -1, -1);
     __syncthreads();
-    constexpr uint32_t shift = 32 - __builtin_ctz(C);
+    jac_stage(ip, ix, u, du, lo, hi, st);
+    constexpr uint32_t shift = 32 - __builtin_ctz(C / 4);
+    constexpr uint32_t mask = C / 4 - 1;
+    int32_t *slots = reinterpret_cast<int32_t *>(tab);
     for (int64_t e = a + threadIdx.x; e < a + du; e += blockDim.x) {
         const int32_t x = ix[e];
         uint32_t h = jac_hash(x) >> shift;
-        while (true) {
-            const int32_t prev = atomicCAS(&tab[h], -1, x);
-            if (prev == -1 || prev == x) break;
-            h = (h + 1) & (C - 1);
+        bool done = false;
+        while (!done) {
+#pragma unroll
+            for (int q = 0; q < 4 && !done; ++q) {
+                const int32_t prev = atomicCAS(&slots[h * 4 + q], -1, x);
+                done = prev == -1 || prev == x;
+            }
+            h = (h + 1) & mask;
         }
     }
     __syncthreads();
-    jac_probe_entries(ip, ix, rev, u, du, lo, hi, out, [&](int32_t x) {
+    jac_probe_staged(ix, rev, du, lo, st, out, [&](int32_t x) {
         uint32_t h = jac_hash(x) >> shift;
         while (true) {
-            const int32_t k = tab[h];
-            if (k == x) return true;
-            if (k == -1) return false;
-            h = (h + 1) & (C - 1);
+            const int4 q = tab[h];
+            if (q.x == x || q.y == x || q.z == x || q.w == x) return true;
+            if (q.w == -1) return false;
+            h = (h + 1) & mask;
         }
     });
 }
@@ -232,7 +312,12 @@ __global__ void __launch_bounds__(1024) k_jac_bitmap(const int64_t *__restrict__
     int64_t a, du, lo, hi;
     jac_task_range(ip, ntask, u, ti[t], a, du, lo, hi);
     const uint32_t *m = bm + (int64_t)(tslot[t] - g0) * words;
-    jac_probe_entries(ip, ix, rev, u, du, lo, hi, out,
+    __shared__ JacStage st;
+    if (threadIdx.x == 0) st.nbig = st.nsmall = 0;
+    __syncthreads();
+    jac_stage(ip, ix, u, du, lo, hi, st);
+    __syncthreads();
+    jac_probe_staged(ix, rev, du, lo, st, out,
                       [&](int32_t x) { return ((m[x >> 5] >> (x & 31)) & 1u) != 0; });
 }
 
@@ -275,7 +360,7 @@ void jaccard_symmetric(gs_ctx *c, double *out) {
     auto *off = (int64_t *)c->buf("jac_off").ensure(sizeof(int64_t) * (n + 1));
     auto *gfl = (int64_t *)c->buf("jac_gflag").ensure(sizeof(int64_t) * (n + 1));
     auto *goff = (int64_t *)c->buf("jac_goff").ensure(sizeof(int64_t) * (n + 1));
-    k_jac_plan<<<grid_for(n, 256, 16384), 256, 0, st>>>(ip, ix, n, cls, ntask);
+    k_jac_plan<<<grid_for(n, 4, 65536), 256, 0, st>>>(ip, ix, n, cls, ntask);
     k_jac_light<<<grid_for(nnz, 256, 65536), 256, 0, st>>>(ip, ix, g.rows.as<int32_t>(), rev, nnz,
                                                            out);
     GS_HIP(hipGetLastError());
