@@ -160,7 +160,7 @@ def main():
 
     from gsparse import graphs
     from gsparse._lib import Context
-    from gsparse.distributed import Comm, sharded_approx_er, sharded_edge_scores, work_ranges
+    from gsparse.distributed import Comm, sharded_approx_er, sharded_edge_scores
     from gsparse.engine import Engine, jl_dim
 
     t_gen = time.perf_counter()
@@ -187,9 +187,7 @@ def main():
     nnz = eng.nnz
     k = jl_dim(n, 0.3)
     comm = Comm(device=dev) if world > 1 else None
-    bounds = None
-    if world > 1 and args.workload == "rmat":
-        bounds = work_ranges(eng.indptr(), ctx.csr()[1], world)
+    bounds = None  # symmetric graphs: Jaccard shards by owner-side pair tasks (gs_jaccard_part)
     jac_out = torch.empty(nnz, dtype=torch.float64, device=dev)
     er_out = torch.empty(nnz, dtype=torch.float64, device=dev)
 

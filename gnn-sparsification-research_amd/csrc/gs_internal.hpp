@@ -171,6 +171,6 @@ void sort_pairs_u64_i64(gs_ctx *c, uint64_t *keys, int64_t *vals, int64_t n, int
 void ensure_transpose(gs_ctx *c);
 
 // Whole-graph Jaccard of a symmetric graph (gs_jaccard.hip)
-void jaccard_symmetric(gs_ctx *c, double *out);
+void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts);
 
 }  // namespace gs

@@ -27,7 +27,8 @@ namespace gs {
 static constexpr int64_t kJacLight = 32;
 static constexpr int64_t kJacGiant = 16384;
 static constexpr int64_t kJacTaskMin = 65536;
-static constexpr int kJacClasses = 4;  // 3 LDS table sizes + bitmap
+static constexpr int kJacClasses = 5;  // 4 LDS table sizes + bitmap
+static constexpr int kJacBitmap = 4;
 static constexpr int kJacUnroll = 4;   // list elements per lane in flight
 static constexpr int kJacMaxEnt = 1024;  // entries per task (LDS staging)
 static constexpr int64_t kJacSmall = 16;  // d_v <= this: 16-lane groups
@@ -45,13 +46,14 @@ __host__ __device__ __forceinline__ int jac_class(int64_t d) {
     if (d <= kJacLight) return -1;
     if (d <= 1024) return 0;
     if (d <= 4096) return 1;
-    if (d <= kJacGiant) return 2;
-    return 3;
+    if (d <= 8192) return 2;
+    if (d <= kJacGiant) return 3;
+    return kJacBitmap;
 }
 
 // probes per task: enough to amortise clearing the C-slot table and the d_u inserts
 __host__ __device__ __forceinline__ int64_t jac_task_probes(int k, int64_t du) {
-    const int64_t tab = k == 0 ? 2048 : k == 1 ? 8192 : k == 2 ? 32768 : 0;
+    const int64_t tab = k == 0 ? 2048 : k == 1 ? 8192 : k == 2 ? 16384 : k == 3 ? 32768 : 0;
     int64_t t = 16 * tab > 8 * du ? 16 * tab : 8 * du;
     return t > kJacTaskMin ? t : kJacTaskMin;
 }
@@ -126,9 +128,9 @@ __global__ void k_jac_emit(const int8_t *__restrict__ cls, const int32_t *__rest
 __global__ void __launch_bounds__(256) k_jac_light(const int64_t *__restrict__ ip,
                                                    const int32_t *__restrict__ ix,
                                                    const int32_t *__restrict__ rows,
-                                                   const int64_t *__restrict__ rev, int64_t nnz,
-                                                   double *__restrict__ out) {
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz;
+                                                   const int64_t *__restrict__ rev, int64_t e0,
+                                                   int64_t e1, double *__restrict__ out) {
+    for (int64_t e = e0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < e1;
          e += (int64_t)gridDim.x * blockDim.x) {
         const int32_t u = rows[e];
         const int64_t a = ip[u], du = ip[u + 1] - a;
@@ -176,13 +178,46 @@ __device__ __forceinline__ void jac_stage(const int64_t *__restrict__ ip,
     }
 }
 
+// Membership tests in two steps, so a lane can have every first read in
+// flight before it resolves any: first(x) issues the read, done(x, s)
+// finishes (following full buckets of the LDS table when it must).
+struct JacHashProbe {
+    const int4 *tab;
+    uint32_t shift, mask;
+    struct S {
+        int4 q;
+        uint32_t h;
+    };
+    __device__ __forceinline__ S first(int32_t x) const {
+        const uint32_t h = jac_hash(x) >> shift;
+        return S{tab[h], h};
+    }
+    __device__ __forceinline__ bool done(int32_t x, S s) const {
+        while (true) {
+            if (s.q.x == x || s.q.y == x || s.q.z == x || s.q.w == x) return true;
+            if (s.q.w == -1) return false;
+            s.h = (s.h + 1) & mask;
+            s.q = tab[s.h];
+        }
+    }
+};
+
+struct JacBitProbe {
+    const uint32_t *m;
+    struct S {
+        uint32_t w;
+    };
+    __device__ __forceinline__ S first(int32_t x) const { return S{m[x >> 5]}; }
+    __device__ __forceinline__ bool done(int32_t x, S s) const { return (s.w >> (x & 31)) & 1u; }
+};
+
 // Probe phase shared by the LDS-table and bitmap kernels (after jac_stage and
 // a barrier).  The d_u of the owner and each entry's d_v give the union.
 template <class Probe>
 __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
                                                  const int64_t *__restrict__ rev, int64_t du,
                                                  int64_t lo, const JacStage &st,
-                                                 double *__restrict__ out, Probe probe) {
+                                                 double *__restrict__ out, const Probe &pr) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     for (int k = wave; k < st.nbig; k += nw) {
         const int64_t b = st.b[k], dv = st.dv[k];
@@ -194,9 +229,12 @@ __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
                 const int64_t j = j0 + t * 64 + lane;
                 xs[t] = j < dv ? ix[b + j] : -1;
             }
+            typename Probe::S ps[kJacUnroll];
+#pragma unroll
+            for (int t = 0; t < kJacUnroll; ++t) ps[t] = pr.first(xs[t] >= 0 ? xs[t] : 0);
 #pragma unroll
             for (int t = 0; t < kJacUnroll; ++t) {
-                const bool hit = xs[t] >= 0 && probe(xs[t]);
+                const bool hit = xs[t] >= 0 && pr.done(xs[t], ps[t]);
                 cnt += __popcll(__ballot(hit));
             }
         }
@@ -215,7 +253,8 @@ __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
         const int k = kJacMaxEnt - 1 - (ok ? idx : 0);
         const int64_t dv = ok ? st.dv[k] : 0;
         const int32_t x = gl < dv ? ix[st.b[k] + gl] : -1;
-        const bool hit = x >= 0 && probe(x);
+        const typename Probe::S ps = pr.first(x >= 0 ? x : 0);
+        const bool hit = x >= 0 && pr.done(x, ps);
         const int64_t cnt = __popcll(__ballot(hit) & gmask);
         if (ok && gl == 0) {
             const int64_t e = lo + st.off[k];
@@ -244,15 +283,16 @@ __global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ i
                                                    const int64_t *__restrict__ rev,
                                                    const int32_t *__restrict__ ntask,
                                                    const int32_t *__restrict__ trow,
-                                                   const int32_t *__restrict__ ti,
+                                                   const int32_t *__restrict__ ti, int64_t t0,
                                                    double *__restrict__ out) {
     // 4-slot buckets (one 16-B LDS read per probe step); a bucket fills from
     // slot 0 up, so a bucket with a free slot 3 ends an unsuccessful search
     __shared__ int4 tab[C / 4];
     __shared__ JacStage st;
-    const int32_t u = trow[blockIdx.x];
+    const int64_t t = t0 + blockIdx.x;
+    const int32_t u = trow[t];
     int64_t a, du, lo, hi;
-    jac_task_range(ip, ntask, u, ti[blockIdx.x], a, du, lo, hi);
+    jac_task_range(ip, ntask, u, ti[t], a, du, lo, hi);
     if (threadIdx.x == 0) st.nbig = st.nsmall = 0;
     for (int s = threadIdx.x; s < C / 4; s += blockDim.x) tab[s] = make_int4(-1, -1, -1, -1);
     __syncthreads();
@@ -274,15 +314,7 @@ __global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ i
         }
     }
     __syncthreads();
-    jac_probe_staged(ix, rev, du, lo, st, out, [&](int32_t x) {
-        uint32_t h = jac_hash(x) >> shift;
-        while (true) {
-            const int4 q = tab[h];
-            if (q.x == x || q.y == x || q.z == x || q.w == x) return true;
-            if (q.w == -1) return false;
-            h = (h + 1) & mask;
-        }
-    });
+    jac_probe_staged(ix, rev, du, lo, st, out, JacHashProbe{tab, shift, mask});
 }
 
 __global__ void k_jac_bitmap_build(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
@@ -317,8 +349,7 @@ __global__ void __launch_bounds__(1024) k_jac_bitmap(const int64_t *__restrict__
     __syncthreads();
     jac_stage(ip, ix, u, du, lo, hi, st);
     __syncthreads();
-    jac_probe_staged(ix, rev, du, lo, st, out,
-                      [&](int32_t x) { return ((m[x >> 5] >> (x & 31)) & 1u) != 0; });
+    jac_probe_staged(ix, rev, du, lo, st, out, JacBitProbe{m});
 }
 
 // B_J for a symmetric graph: 8 * sum_u d_u^2 + 12 * nnz
@@ -334,12 +365,17 @@ __global__ void k_jac_bytes(const int64_t *__restrict__ ip, int64_t n,
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(acc, s);
 }
 
-// Whole-graph Jaccard of a symmetric graph into device out[nnz].
-void jaccard_symmetric(gs_ctx *c, double *out) {
+// Whole-graph Jaccard of a symmetric graph into device out[nnz], or part
+// `part` of `nparts` of it: that part's share of the light entries and of
+// every class's task list (both CSR entries of each pair written), every
+// other entry 0.0 -- the nparts outputs sum to the whole.
+void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts) {
     Graph &g = c->g;
     const int64_t n = g.n, nnz = g.nnz;
     if (!nnz) return;
     hipStream_t st = c->stream;
+    auto share = [&](int64_t total, int p) { return total * p / nparts; };
+    if (nparts > 1) GS_HIP(hipMemsetAsync(out, 0, sizeof(double) * nnz, st));
     const int64_t *ip = g.indptr.as<int64_t>();
     const int32_t *ix = g.indices.as<int32_t>();
     const int64_t *rev = g.tpos.as<int64_t>();
@@ -361,11 +397,15 @@ void jaccard_symmetric(gs_ctx *c, double *out) {
     auto *gfl = (int64_t *)c->buf("jac_gflag").ensure(sizeof(int64_t) * (n + 1));
     auto *goff = (int64_t *)c->buf("jac_goff").ensure(sizeof(int64_t) * (n + 1));
     k_jac_plan<<<grid_for(n, 4, 65536), 256, 0, st>>>(ip, ix, n, cls, ntask);
-    k_jac_light<<<grid_for(nnz, 256, 65536), 256, 0, st>>>(ip, ix, g.rows.as<int32_t>(), rev, nnz,
-                                                           out);
+    {
+        const int64_t e0 = share(nnz, part), e1 = share(nnz, part + 1);
+        if (e1 > e0)
+            k_jac_light<<<grid_for(e1 - e0, 256, 65536), 256, 0, st>>>(
+                ip, ix, g.rows.as<int32_t>(), rev, e0, e1, out);
+    }
     GS_HIP(hipGetLastError());
     for (int k = 0; k < kJacClasses; ++k) {
-        const bool giant = k == 3;
+        const bool giant = k == kJacBitmap;
         GS_HIP(hipMemsetAsync(cnt + n, 0, sizeof(int64_t), st));
         GS_HIP(hipMemsetAsync(gfl + n, 0, sizeof(int64_t), st));
         k_jac_mask<<<grid_for(n, 256, 16384), 256, 0, st>>>(cls, ntask, n, k, cnt,
@@ -388,13 +428,17 @@ void jaccard_symmetric(gs_ctx *c, double *out) {
                                                             n, k, trow, ti, tslot, grow);
         GS_HIP(hipGetLastError());
         GS_CHECK(ntot <= INT32_MAX, GS_EUNSUPPORTED, "too many Jaccard tasks (%lld)", (long long)ntot);
-        const unsigned nb = (unsigned)ntot;
+        const int64_t tlo = share(ntot, part), thi = share(ntot, part + 1);
+        const unsigned nb = (unsigned)(thi - tlo);
+        if (k < kJacBitmap && !nb) continue;
         if (k == 0) {
-            k_jac_hash<2048><<<nb, 256, 0, st>>>(ip, ix, rev, ntask, trow, ti, out);
+            k_jac_hash<2048><<<nb, 256, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out);
         } else if (k == 1) {
-            k_jac_hash<8192><<<nb, 512, 0, st>>>(ip, ix, rev, ntask, trow, ti, out);
+            k_jac_hash<8192><<<nb, 512, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out);
         } else if (k == 2) {
-            k_jac_hash<32768><<<nb, 1024, 0, st>>>(ip, ix, rev, ntask, trow, ti, out);
+            k_jac_hash<16384><<<nb, 1024, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out);
+        } else if (k == 3) {
+            k_jac_hash<32768><<<nb, 1024, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out);
         } else {
             // bitmaps in batches of rows (<= 1 GiB of bits at a time)
             const int64_t words = (n + 31) / 32;
@@ -413,6 +457,10 @@ void jaccard_symmetric(gs_ctx *c, double *out) {
                     GS_HIP(hipMemcpyAsync(&tb[1], off + hrow[g1], 8, hipMemcpyDeviceToHost, st));
                 GS_HIP(hipStreamSynchronize(st));
                 if (g1 >= ngiant) tb[1] = ntot;
+                // this part's tasks only
+                if (tb[0] < tlo) tb[0] = tlo;
+                if (tb[1] > thi) tb[1] = thi;
+                if (tb[1] <= tb[0]) continue;
                 auto *bm = (uint32_t *)c->buf("jac_bitmap").ensure(sizeof(uint32_t) * words * (g1 - g0));
                 GS_HIP(hipMemsetAsync(bm, 0, sizeof(uint32_t) * words * (g1 - g0), st));
                 k_jac_bitmap_build<<<dim3(64, (unsigned)(g1 - g0)), 256, 0, st>>>(

@@ -240,7 +240,7 @@ int gs_jaccard(gs_ctx *c, int64_t e0, int64_t e1, double *out, int loc) {
         const char *mode = getenv("GSPARSE_JACCARD");
         const bool merge_only = mode && strcmp(mode, "merge") == 0;
         if (cnt && g.symmetric && e0 == 0 && e1 == g.nnz && !merge_only) {
-            jaccard_symmetric(c, dout);  // owner-side hash/bitmap probing, both entries written
+            jaccard_symmetric(c, dout, 0, 1);  // owner-side hash/bitmap probing, both entries written
         } else if (cnt) {
             const int64_t *tp = g.symmetric ? g.indptr.as<int64_t>() : g.tptr.as<int64_t>();
             const int32_t *ti = g.symmetric ? g.indices.as<int32_t>() : g.tidx.as<int32_t>();
@@ -253,6 +253,33 @@ int gs_jaccard(gs_ctx *c, int64_t e0, int64_t e1, double *out, int loc) {
             prof_end(c, t0, "jaccard", 0.0);
         }
         finish_out(c, out, dout, sizeof(double) * cnt, loc);
+    });
+}
+
+int gs_jaccard_part(gs_ctx *c, int part, int nparts, double *out, int loc) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        GS_CHECK(nparts >= 1 && 0 <= part && part < nparts, GS_EINVAL, "bad part %d of %d", part,
+                 nparts);
+        GS_HIP(hipSetDevice(c->device));
+        Graph &g = c->g;
+        const int64_t nnz = g.nnz;
+        double *dout = (double *)out_device(c, c->outbuf, out, sizeof(double) * nnz, loc);
+        if (nnz && g.symmetric) {
+            jaccard_symmetric(c, dout, part, nparts);
+        } else if (nnz) {  // directed: this part's edge range, zeros elsewhere
+            const int64_t e0 = nnz * part / nparts, e1 = nnz * (part + 1) / nparts;
+            GS_HIP(hipMemsetAsync(dout, 0, sizeof(double) * nnz, c->stream));
+            if (e1 > e0) {
+                hipEvent_t t0 = prof_begin(c);
+                k_jaccard<<<grid_for(e1 - e0, 256), 256, 0, c->stream>>>(
+                    g.indptr.as<int64_t>(), g.indices.as<int32_t>(), g.rows.as<int32_t>(),
+                    g.tptr.as<int64_t>(), g.tidx.as<int32_t>(), e0, e1, dout + e0);
+                GS_HIP(hipGetLastError());
+                prof_end(c, t0, "jaccard", 0.0);
+            }
+        }
+        finish_out(c, out, dout, sizeof(double) * nnz, loc);
     });
 }
 

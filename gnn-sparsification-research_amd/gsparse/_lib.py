@@ -44,6 +44,7 @@ SIGNATURES = {
     "gs_graph_shape": (_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64), ctypes.POINTER(_int)]),
     "gs_graph_copy_csr": (_int, [_vp, _vp, _vp, _vp, _int]),
     "gs_jaccard": (_int, [_vp, _i64, _i64, _vp, _int]),
+    "gs_jaccard_part": (_int, [_vp, _int, _int, _vp, _int]),
     "gs_adamic_adar": (_int, [_vp, _vp, _int, _i64, _i64, _vp, _int]),
     "gs_degree": (_int, [_vp, _i64, _i64, _vp, _int]),
     "gs_feature_cosine_f32": (_int, [_vp, _vp, _i64, _int, _i64, _i64, _vp, _int]),

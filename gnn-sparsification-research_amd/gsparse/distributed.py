@@ -1,9 +1,14 @@
 """Multi-GPU sharding of the scorers (one process per GPU, torch.distributed).
 
 SURVEY §8(e):
-  * Jaccard / AA / degree / FeatCos: contiguous CSR edge ranges (equal
-    counts, or equal per-edge work d_u + d_v for skewed graphs), then an
-    all-gather of the fp64 scores so every rank can run the global top-k.
+  * Jaccard on a symmetric graph: each rank takes its share of the owner-side
+    pair tasks (gs_jaccard_part: both CSR entries of a pair, zeros elsewhere)
+    and one all-reduce(sum) assembles the whole vector -- exact, since every
+    entry has exactly one non-zero contributor.
+  * AA / degree / FeatCos (and Jaccard on explicit ranges): contiguous CSR
+    edge ranges (equal counts, or equal per-edge work d_u + d_v for skewed
+    graphs), then an all-gather of the fp64 scores so every rank can run the
+    global top-k.
   * ApproxER: the k JL columns are independent CG solves.  Rank blocks are
     nodes of NumPy's pairwise-sum tree over k (gs_er_split), so each rank's
     per-edge partial sum is exactly a subtree of the reference's
@@ -88,6 +93,11 @@ class Comm:
         dist.all_gather(out, buf, group=self.group)
         return torch.cat([out[r][: sizes[r]] for r in range(self.world)])
 
+    def all_reduce_sum(self, local: torch.Tensor) -> torch.Tensor:
+        t = local.to(self.device).clone()
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
     def all_gather_same(self, local: torch.Tensor) -> list[torch.Tensor]:
         out = [torch.empty_like(local, device=self.device) for _ in range(self.world)]
         dist.all_gather(out, local.to(self.device), group=self.group)
@@ -98,6 +108,12 @@ def sharded_edge_scores(engine, comm: Comm, metric: str, bounds: list[int] | Non
                         **kw):
     """One scorer over this rank's CSR edge range, all-gathered to every rank."""
     nnz = engine.nnz
+    if metric == "jaccard" and bounds is None and hasattr(engine, "jaccard_part"):
+        out = None
+        if comm.device.type == "cuda":
+            out = torch.empty(nnz, dtype=torch.float64, device=comm.device)
+        part = engine.jaccard_part(comm.rank, comm.world, out=out)
+        return comm.all_reduce_sum(comm.tensor(part))
     b = bounds or edge_ranges(nnz, comm.world)
     e0, e1 = b[comm.rank], b[comm.rank + 1]
     fn = {"jaccard": engine.jaccard, "adamic_adar": engine.adamic_adar,

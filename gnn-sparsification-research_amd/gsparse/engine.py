@@ -90,6 +90,13 @@ class Engine:
         self.ctx.call("gs_jaccard", e0, e1, ptr(o), loc)
         return o
 
+    def jaccard_part(self, part: int, nparts: int, out=None):
+        """Share `part` of `nparts` of the whole Jaccard vector (zeros elsewhere;
+        the shares sum to jaccard()) -- gs_jaccard_part."""
+        o, loc = self._out(0, self.nnz, out)
+        self.ctx.call("gs_jaccard_part", part, nparts, ptr(o), loc)
+        return o
+
     def adamic_adar(self, e0: int = 0, e1: int | None = None, out=None, c=None):
         e1 = self.nnz if e1 is None else e1
         if c is None:

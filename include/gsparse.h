@@ -77,6 +77,12 @@ int gs_graph_copy_csr(gs_ctx *ctx, int64_t *indptr, int32_t *indices, double *da
 /* ---- scorers: out[e - e0] for CSR entries e in [e0, e1) ------------------ */
 /* calculate_jaccard_scores, metrics.py:17-64 (bit-exact). */
 int gs_jaccard(gs_ctx *ctx, int64_t e0, int64_t e1, double *out, int loc);
+/* Part `part` of `nparts` of the whole-graph Jaccard (multi-GPU sharding,
+ * SURVEY 8(e)): out[nnz] holds this part's pairs (both CSR entries of each
+ * undirected pair on a symmetric graph; an edge range on a directed one) and
+ * 0.0 elsewhere, so the element-wise sum of the nparts outputs equals
+ * gs_jaccard(0, nnz) bit for bit. */
+int gs_jaccard_part(gs_ctx *ctx, int part, int nparts, double *out, int loc);
 /* calculate_adamic_adar_scores, metrics.py:67-121 (bit-exact).  c[w] =
  * 1/sqrt(max(log(deg_w+1),1e-10)) as NumPy computes it (metrics.py:104-108),
  * n values. */

@@ -29,6 +29,11 @@ class OracleEngine:
             self._jac = O.jaccard(self.ip, self.ix)
         return self._jac[e0:e1]
 
+    def jaccard_part(self, part, nparts, out=None):
+        full = self.jaccard()
+        keep = (np.arange(self.nnz) % nparts) == part
+        return np.where(keep, full, 0.0)
+
     def degree(self, e0=0, e1=None, out=None):
         return O.degree(self.ip, self.ix, self.d)[e0:e1]
 

@@ -201,6 +201,27 @@ def test_jaccard_owner_hash_classes_vs_oracle(gs, monkeypatch):
     assert bits_equal(e.jaccard(), ref)
 
 
+@pytest.mark.parametrize("nparts", [1, 2, 3, 8])
+def test_jaccard_parts_sum_to_whole(gs, nparts):
+    ei, n = _hub_graph()
+    data = gs.Data(edge_index=torch.from_numpy(ei), num_nodes=n)
+    e = gs.GraphSparsifier(data, "cpu")._engine
+    whole = e.jaccard()
+    parts = [e.jaccard_part(p, nparts) for p in range(nparts)]
+    tot = np.zeros_like(whole)
+    for p in parts:
+        tot = tot + p
+    assert bits_equal(tot, whole)
+    # every entry has exactly one contributing part
+    assert np.array_equal(sum((p != 0).astype(int) for p in parts), (whole != 0).astype(int))
+    # directed graph: edge ranges
+    g = load_golden("directed_dup")
+    d = gs.Data(edge_index=torch.from_numpy(g["edge_index"]), num_nodes=int(g["num_nodes"]))
+    ed = gs.GraphSparsifier(d, "cpu")._engine
+    tot = sum(ed.jaccard_part(p, nparts) for p in range(nparts))
+    assert bits_equal(tot, g["scores_jaccard"])
+
+
 def test_backbone_rmat12_vs_oracle(gs):
     from gsparse import graphs
 
