@@ -569,53 +569,91 @@ __global__ void __launch_bounds__(256) k_dot_acc(CgGeom G, ChunkArg ch,
         if (c + u < G.col1) acc[((c + u - G.col0) * kMaxChunks + ln.t) * 32 + ln.j] = s[u];
 }
 
-// OpenBLAS ddot finish for one column: 32 chains -> value (see oracle_ddot).
-// Values of the (< 32) leftover rows of chunk t are A[row] and, when
-// Bside != nullptr, Bside[(t*32 + row - a - n32) * ld] (else B[row]).
-__device__ __noinline__ double ddot_finish(const double *__restrict__ acc_c, const ChunkArg &ch, int64_t ld,
-                              int64_t c, const double *__restrict__ A,
-                              const double *__restrict__ B, const double *__restrict__ Bside) {
-    double total = 0.0;
-    for (int t = 0; t < ch.count; ++t) {
-        const int64_t a = ch.a[t], L = ch.len[t];
-        const int64_t n1 = L & ~(int64_t)15, n32 = n1 & ~(int64_t)31;
-        double dot = 0.0;
-        if (n1) {
-            const double *a32 = acc_c + t * 32;
-            double b[16];
-            for (int q = 0; q < 4; ++q)
-                for (int l = 0; l < 4; ++l) b[4 * q + l] = a32[8 * q + l] + a32[8 * q + 4 + l];
-            if (n1 > n32) {
-                for (int jj = 0; jj < 16; ++jj) {
-                    int64_t row = a + n32 + jj;
-                    double bv = Bside ? Bside[((int64_t)t * 32 + (row - a - n32)) * ld + c]
-                                      : B[row * ld + c];
-                    b[jj] = __builtin_fma(A[row * ld + c], bv, b[jj]);
-                }
+// OpenBLAS ddot finish (see oracle_ddot), one wave per column, one lane per
+// BLAS chunk t: fold of the chunk's 32 chains, its optional 16-row block and
+// FMA tail, then the chunk dots added in order from 0.0 (a single chunk is
+// returned as is).  Values of the (< 32) leftover rows of chunk t are A[row]
+// and, when Bside != nullptr, Bside[(t*32 + row - a - n32) * ld] (else B[row]).
+__device__ __forceinline__ double chunk_dot(const double *__restrict__ a32, int64_t a, int64_t L,
+                                            int t, int64_t ld, int64_t c,
+                                            const double *__restrict__ A,
+                                            const double *__restrict__ B,
+                                            const double *__restrict__ Bside) {
+    const int64_t n1 = L & ~(int64_t)15, n32 = n1 & ~(int64_t)31;
+    auto bval = [&](int64_t row) {
+        return Bside ? Bside[((int64_t)t * 32 + (row - a - n32)) * ld + c] : B[row * ld + c];
+    };
+    double dot = 0.0;
+    if (n1) {
+        double b[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int l = 0; l < 4; ++l) b[4 * q + l] = a32[8 * q + l] + a32[8 * q + 4 + l];
+        if (n1 > n32) {
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+                const int64_t row = a + n32 + jj;
+                b[jj] = __builtin_fma(A[row * ld + c], bval(row), b[jj]);
             }
-            double c4[4];
-            for (int l = 0; l < 4; ++l) c4[l] = ((b[l] + b[4 + l]) + b[8 + l]) + b[12 + l];
-            dot = (c4[0] + c4[2]) + (c4[1] + c4[3]);
         }
-        for (int64_t i = a + n1; i < a + L; ++i) {
-            double bv = Bside ? Bside[((int64_t)t * 32 + (i - a - n32)) * ld + c] : B[i * ld + c];
-            dot = __builtin_fma(bv, A[i * ld + c], dot);
-        }
-        if (ch.count == 1) return dot;
-        total = total + dot;
+        double c4[4];
+#pragma unroll
+        for (int l = 0; l < 4; ++l) c4[l] = ((b[l] + b[4 + l]) + b[8 + l]) + b[12 + l];
+        dot = (c4[0] + c4[2]) + (c4[1] + c4[3]);
     }
+    double tv[15], ta[15];  // tail loads first, then the dependent FMA chain
+#pragma unroll
+    for (int i = 0; i < 15; ++i) {
+        const int64_t row = a + n1 + i;
+        const bool in = row < a + L;
+        tv[i] = in ? bval(row) : 0.0;
+        ta[i] = in ? A[row * ld + c] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 15; ++i)
+        if (n1 + i < L) dot = __builtin_fma(tv[i], ta[i], dot);
+    return dot;
+}
+
+// value of column c's dot product; call with the whole wave (lane = chunk)
+__device__ __noinline__ double ddot_finish_wave(const double *__restrict__ acc_c,
+                                                   const int64_t *__restrict__ ca,
+                                                   const int64_t *__restrict__ cl, int count,
+                                                   int64_t ld, int64_t c,
+                                                   const double *__restrict__ A,
+                                                   const double *__restrict__ B,
+                                                   const double *__restrict__ Bside) {
+    const int lane = threadIdx.x & 63;
+    double d = 0.0;
+    if (lane < count) d = chunk_dot(acc_c + lane * 32, ca[lane], cl[lane], lane, ld, c, A, B, Bside);
+    if (count == 1) return __shfl(d, 0);
+    double total = 0.0;
+    for (int t = 0; t < count; ++t) total = total + __shfl(d, t);
     return total;
 }
 
+// one wave per column: c = col0 + blockIdx.x * waves + wave
+__device__ __forceinline__ int64_t fin_column(const CgGeom &G) {
+    return G.col0 + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+}
+
 // init: rho = b.b, bn = sqrt(rho), atol = rtol*bn; bn == 0 -> done (x = b)
-__global__ void k_fin_init(CgGeom G, ChunkArg ch, const double *__restrict__ acc,
-                           const double *__restrict__ Rr, double rtol, double *__restrict__ bn,
-                           double *__restrict__ atol, double *__restrict__ rho,
-                           int32_t *__restrict__ active, int32_t *__restrict__ iters,
-                           int32_t *__restrict__ xstep, int32_t *__restrict__ nactive) {
-    int64_t c = G.col0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(256) k_fin_init(CgGeom G, const int64_t *__restrict__ ca,
+                                                  const int64_t *__restrict__ cl, int count,
+                                                  const double *__restrict__ acc,
+                                                  const double *__restrict__ Rr, double rtol,
+                                                  double *__restrict__ bn, double *__restrict__ atol,
+                                                  double *__restrict__ rho,
+                                                  int32_t *__restrict__ active,
+                                                  int32_t *__restrict__ iters,
+                                                  int32_t *__restrict__ xstep,
+                                                  int32_t *__restrict__ nactive) {
+    const int64_t c = fin_column(G);
     if (c >= G.col1) return;
-    double d = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.ld, c, Rr, Rr, nullptr);
+    const double d = ddot_finish_wave(acc + (c - G.col0) * kMaxChunks * 32, ca, cl, count, G.ld, c,
+                                      Rr, Rr, nullptr);
+    if ((threadIdx.x & 63) != 0) return;
     double b = __builtin_sqrt(d);
     bn[c] = b;
     double at = rtol * b;  // max(atol=0, rtol*bnrm2)
@@ -630,26 +668,40 @@ __global__ void k_fin_init(CgGeom G, ChunkArg ch, const double *__restrict__ acc
     if (act) atomicAdd(nactive, 1);
 }
 
-__global__ void k_fin_pq(CgGeom G, ChunkArg ch, const double *__restrict__ acc,
-                         const double *__restrict__ P, const double *__restrict__ qside,
-                         const double *__restrict__ rho, const int32_t *__restrict__ active,
-                         int32_t it, double *__restrict__ alpha, int32_t *__restrict__ xstep) {
-    int64_t c = G.col0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(256) k_fin_pq(CgGeom G, const int64_t *__restrict__ ca,
+                                                const int64_t *__restrict__ cl, int count,
+                                                const double *__restrict__ acc,
+                                                const double *__restrict__ P,
+                                                const double *__restrict__ qside,
+                                                const double *__restrict__ rho,
+                                                const int32_t *__restrict__ active, int32_t it,
+                                                double *__restrict__ alpha,
+                                                int32_t *__restrict__ xstep) {
+    const int64_t c = fin_column(G);
     if (c >= G.col1 || !active[c]) return;
-    double pq = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.ld, c, P, nullptr, qside);
+    const double pq = ddot_finish_wave(acc + (c - G.col0) * kMaxChunks * 32, ca, cl, count, G.ld,
+                                       c, P, nullptr, qside);
+    if ((threadIdx.x & 63) != 0) return;
     alpha[c] = rho[c] / pq;
     xstep[c] = it;  // x += alpha p is applied by the next k_cg_pq (or the flush)
 }
 
 // after the update of iteration `it`: rho_prev = rho; rho = r.r; loop-top test
-__global__ void k_fin_rr(CgGeom G, ChunkArg ch, const double *__restrict__ acc,
-                         const double *__restrict__ Rr, int32_t it, double *__restrict__ rho,
-                         double *__restrict__ rho_prev, const double *__restrict__ atol,
-                         int32_t *__restrict__ active, int32_t *__restrict__ iters,
-                         int32_t *__restrict__ nactive) {
-    int64_t c = G.col0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(256) k_fin_rr(CgGeom G, const int64_t *__restrict__ ca,
+                                                const int64_t *__restrict__ cl, int count,
+                                                const double *__restrict__ acc,
+                                                const double *__restrict__ Rr, int32_t it,
+                                                double *__restrict__ rho,
+                                                double *__restrict__ rho_prev,
+                                                const double *__restrict__ atol,
+                                                int32_t *__restrict__ active,
+                                                int32_t *__restrict__ iters,
+                                                int32_t *__restrict__ nactive) {
+    const int64_t c = fin_column(G);
     if (c >= G.col1 || !active[c]) return;
-    double rr = ddot_finish(acc + (c - G.col0) * kMaxChunks * 32, ch, G.ld, c, Rr, Rr, nullptr);
+    const double rr = ddot_finish_wave(acc + (c - G.col0) * kMaxChunks * 32, ca, cl, count, G.ld,
+                                       c, Rr, Rr, nullptr);
+    if ((threadIdx.x & 63) != 0) return;
     rho_prev[c] = rho[c];
     rho[c] = rr;
     iters[c] = it + 1;
@@ -853,7 +905,16 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         double *acc = er.acc.as<double>();
         // 8 workgroups (32 residues) per (column block, chunk) pair, XCD-grouped
         dim3 grid((unsigned)(((G.npairs + 7) / 8) * 64)), block(256);
-        unsigned fgrid = grid_for(ncols, 64);
+        // finish kernels: one wave per column, one lane per BLAS chunk
+        const unsigned fgrid = grid_for(ncols, 4);
+        int64_t hch[2 * kMaxChunks];
+        for (int t = 0; t < ch.count; ++t) {
+            hch[t] = ch.a[t];
+            hch[kMaxChunks + t] = ch.len[t];
+        }
+        auto *dch = (int64_t *)c->buf("er_chunks").ensure(sizeof(hch));
+        GS_HIP(hipMemcpyAsync(dch, hch, sizeof(hch), hipMemcpyHostToDevice, c->stream));
+        const int64_t *ca = dch, *cl = dch + kMaxChunks;
         // algorithmic bytes: pq reads x, p, r and writes x, p (first iteration: r in, p out);
         // upd reads p, r and writes r
         const double bytes_pq = 40.0 * n * ncols, bytes_pq0 = 16.0 * n * ncols,
@@ -865,8 +926,9 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         // ||b|| and rho_0 (r = b.copy())
         if (cpl == 2) k_dot_acc<2><<<grid, block, 0, c->stream>>>(G, ch, Rr, Rr, acc);
         else k_dot_acc<1><<<grid, block, 0, c->stream>>>(G, ch, Rr, Rr, acc);
-        k_fin_init<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Rr, rtol, cp.bn, cp.atol, cp.rho,
-                                                 cp.active, cp.iters, cp.xstep, cp.nactive);
+        k_fin_init<<<fgrid, 256, 0, c->stream>>>(G, ca, cl, ch.count, acc, Rr, rtol, cp.bn,
+                                                  cp.atol, cp.rho, cp.active, cp.iters, cp.xstep,
+                                                  cp.nactive);
         if (n)
             k_x_init<<<grid_for(n * ncols, 256, 65536), 256, 0, c->stream>>>(G, Rr, cp.bn, X);
         GS_HIP(hipGetLastError());
@@ -893,7 +955,8 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             }
 #undef GS_PQ
             prof_end(c, t0, "cg_pq", it == 0 ? bytes_pq0 : bytes_pq);
-            k_fin_pq<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Pnew, qside, cp.rho, cp.active, it,
+            k_fin_pq<<<fgrid, 256, 0, c->stream>>>(G, ca, cl, ch.count, acc, Pnew, qside, cp.rho,
+                                                   cp.active, it,
                                                   cp.alpha, cp.xstep);
             t0 = prof_begin(c);
             if (cpl == 2)
@@ -903,7 +966,8 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
                 k_cg_upd<1><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Pnew, Rr, cp.alpha,
                                                            cp.active, acc);
             prof_end(c, t0, "cg_upd", bytes_upd);
-            k_fin_rr<<<fgrid, 64, 0, c->stream>>>(G, ch, acc, Rr, it, cp.rho, cp.rho_prev, cp.atol,
+            k_fin_rr<<<fgrid, 256, 0, c->stream>>>(G, ca, cl, ch.count, acc, Rr, it, cp.rho,
+                                                   cp.rho_prev, cp.atol,
                                                   cp.active, cp.iters, cp.nactive);
             GS_HIP(hipGetLastError());
             cur ^= 1;

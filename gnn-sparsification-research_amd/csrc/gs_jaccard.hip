@@ -62,10 +62,12 @@ __host__ __device__ __forceinline__ int64_t jac_task_probes(int k, int64_t du) {
 __global__ void __launch_bounds__(256) k_jac_plan(const int64_t *__restrict__ ip,
                                                   const int32_t *__restrict__ ix, int64_t n,
                                                   int8_t *__restrict__ cls,
-                                                  int32_t *__restrict__ ntask) {
+                                                  int32_t *__restrict__ ntask,
+                                                  unsigned long long *__restrict__ tot) {
     const int lane = threadIdx.x & 63;
     const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    unsigned long long mine[kJacClasses + 1] = {};  // lane 0: this wave's task totals
     for (int64_t u = w0; u < n; u += nw) {
         const int64_t a = ip[u], du = ip[u + 1] - a;
         const int k = jac_class(du);
@@ -89,8 +91,22 @@ __global__ void __launch_bounds__(256) k_jac_plan(const int64_t *__restrict__ ip
             }
             cls[u] = (int8_t)k;
             ntask[u] = (int32_t)nt;
+            if (nt) {  // per-class task totals; [kJacClasses] = rows with bitmap tasks
+#pragma unroll
+                for (int q = 0; q < kJacClasses; ++q) mine[q] += q == k ? (unsigned long long)nt : 0ull;
+                mine[kJacClasses] += k == kJacBitmap ? 1ull : 0ull;
+            }
         }
     }
+    __shared__ unsigned long long red[kJacClasses + 1];
+    if (threadIdx.x < kJacClasses + 1) red[threadIdx.x] = 0;
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q <= kJacClasses; ++q)
+            if (mine[q]) atomicAdd(&red[q], mine[q]);
+    __syncthreads();
+    if (threadIdx.x < kJacClasses + 1 && red[threadIdx.x]) atomicAdd(&tot[threadIdx.x], red[threadIdx.x]);
 }
 
 __global__ void k_jac_mask(const int8_t *__restrict__ cls, const int32_t *__restrict__ ntask,
@@ -396,7 +412,9 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts) {
     auto *off = (int64_t *)c->buf("jac_off").ensure(sizeof(int64_t) * (n + 1));
     auto *gfl = (int64_t *)c->buf("jac_gflag").ensure(sizeof(int64_t) * (n + 1));
     auto *goff = (int64_t *)c->buf("jac_goff").ensure(sizeof(int64_t) * (n + 1));
-    k_jac_plan<<<grid_for(n, 4, 65536), 256, 0, st>>>(ip, ix, n, cls, ntask);
+    auto *dtot = (unsigned long long *)c->buf("jac_tot").ensure(8 * (kJacClasses + 1));
+    GS_HIP(hipMemsetAsync(dtot, 0, 8 * (kJacClasses + 1), st));
+    k_jac_plan<<<grid_for(n, 4, 4096), 256, 0, st>>>(ip, ix, n, cls, ntask, dtot);
     {
         const int64_t e0 = share(nnz, part), e1 = share(nnz, part + 1);
         if (e1 > e0)
@@ -404,22 +422,24 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts) {
                 ip, ix, g.rows.as<int32_t>(), rev, e0, e1, out);
     }
     GS_HIP(hipGetLastError());
+    unsigned long long htot[kJacClasses + 1];
+    GS_HIP(hipMemcpyAsync(htot, dtot, sizeof(htot), hipMemcpyDeviceToHost, st));
+    GS_HIP(hipStreamSynchronize(st));  // the only sync unless bitmap rows exist
+    int64_t tmax = 1;
+    for (int k = 0; k < kJacClasses; ++k) tmax = (int64_t)htot[k] > tmax ? (int64_t)htot[k] : tmax;
+    // task lists are reused class after class (stream order): size them once
+    auto *trow = (int32_t *)c->buf("jac_trow").ensure(sizeof(int32_t) * tmax);
+    auto *ti = (int32_t *)c->buf("jac_ti").ensure(sizeof(int32_t) * tmax);
     for (int k = 0; k < kJacClasses; ++k) {
         const bool giant = k == kJacBitmap;
+        const int64_t ntot = (int64_t)htot[k], ngiant = giant ? (int64_t)htot[kJacClasses] : 0;
+        if (!ntot) continue;
         GS_HIP(hipMemsetAsync(cnt + n, 0, sizeof(int64_t), st));
         GS_HIP(hipMemsetAsync(gfl + n, 0, sizeof(int64_t), st));
         k_jac_mask<<<grid_for(n, 256, 16384), 256, 0, st>>>(cls, ntask, n, k, cnt,
                                                             giant ? gfl : nullptr);
         exclusive_scan_i64(c, cnt, off, n + 1);
         if (giant) exclusive_scan_i64(c, gfl, goff, n + 1);
-        int64_t tot[2] = {0, 0};
-        GS_HIP(hipMemcpyAsync(&tot[0], off + n, 8, hipMemcpyDeviceToHost, st));
-        if (giant) GS_HIP(hipMemcpyAsync(&tot[1], goff + n, 8, hipMemcpyDeviceToHost, st));
-        GS_HIP(hipStreamSynchronize(st));
-        const int64_t ntot = tot[0], ngiant = tot[1];
-        if (!ntot) continue;
-        auto *trow = (int32_t *)c->buf("jac_trow").ensure(sizeof(int32_t) * ntot);
-        auto *ti = (int32_t *)c->buf("jac_ti").ensure(sizeof(int32_t) * ntot);
         int32_t *tslot = giant ? (int32_t *)c->buf("jac_tslot").ensure(sizeof(int32_t) * ntot)
                                : nullptr;
         int32_t *grow = giant ? (int32_t *)c->buf("jac_grow").ensure(sizeof(int32_t) * ngiant)
