@@ -3,13 +3,18 @@
 //
 // Layout in HBM (row-major n x k, the JL columns contiguous per node):
 //   Rr  residual, initialised with Y = B @ R           (metrics.py:275)
-//   X   solution, P0/P1 search direction (ping-pong), Q = L_reg p
+//   X   solution, P0/P1 search direction (ping-pong), Q = L_reg p (whole in
+//       modes 1-3, else only the leftover rows of each BLAS chunk)
 // The k CG solves (metrics.py:284-289, SciPy 1.15 cg recurrence) run as one
-// batched iteration: per iteration two fused streaming kernels
-//   k_cg_pq : p = beta*p + r (two roundings) ; q = L_reg p (per-row fold from
-//             0.0 in ascending column, products rounded) ; partial dot(p,q)
-//   k_cg_upd: x += fl(alpha p) ; r -= fl(alpha q) ; partial dot(r,r)
-// plus two per-column finish kernels.  Every dot product reproduces
+// batched iteration.  Short rows (mode 0), two fused kernels per iteration:
+//   k_cg_pq : x += fl(alpha_{t-1} p_{t-1}) (deferred x update of the previous
+//             iteration); p = beta*p + r (two roundings), neighbours' p
+//             recomputed; q = L_reg p (per-row fold from 0.0 in ascending
+//             column, products rounded); partial dot(p,q)
+//   k_cg_upd: q recomputed from the stored p; r -= fl(alpha q); partial dot(r,r)
+// (64 B per entry and iteration).  Long rows (mode 3): k_cg_p (p stream),
+// k_spmv (column-block-major SpMV, q stored), k_dot_acc, k_cg_upd<STOREQ>.
+// Plus two per-column finish kernels.  Every dot product reproduces
 // OpenBLAS ddot (SkylakeX kernel) as np.dot calls it: T thread chunks for
 // n > 10000, inside a chunk 32 FMA accumulator chains over rows j, j+32, ...,
 // then the 32->16 fold, the optional 16-block, the 4-lane tree and the FMA
@@ -22,6 +27,7 @@
 namespace gs {
 
 static constexpr int kMaxChunks = 64;
+static constexpr int64_t kStoreQRowLen = 8;  // L_reg entries per row above which q is stored
 
 struct Chunks {
     int32_t count;
@@ -319,7 +325,7 @@ struct Vec<2> {
 //   p_t = fl(fl(beta_t p_{t-1}) + r_t)  (own row stored; neighbours recomputed)
 //   q_t = L_reg p_t (per-row fold from 0.0, ascending column), kept only for the
 //         <32 leftover rows the ddot finish needs (qside); chains of dot(p_t, q_t).
-template <bool FIRST, int CPL>
+template <bool FIRST, int CPL, bool STOREQ>
 __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
                                                const int64_t *__restrict__ lp,
                                                const int32_t *__restrict__ li,
@@ -328,6 +334,7 @@ __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
                                                const double *__restrict__ Pold,
                                                double *__restrict__ Pnew, double *__restrict__ X,
                                                double *__restrict__ qside,
+                                               double *__restrict__ Q,
                                                const double *__restrict__ rho,
                                                const double *__restrict__ rho_prev,
                                                const double *__restrict__ alpha,
@@ -424,6 +431,18 @@ __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
             for (int u = 0; u < CPL; ++u)
                 if (live[u]) Pnew[row * ld + c + u] = pi[u];
         }
+        if (STOREQ) {  // high-degree graphs: q kept, the update kernel streams it
+            Vec<CPL> qw;
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) qw.v[u] = q[u];
+            if (CPL == 1 || (live[0] && live[CPL - 1])) {
+                qw.store(Q + row * ld + c);
+            } else {
+#pragma unroll
+                for (int u = 0; u < CPL; ++u)
+                    if (live[u]) Q[row * ld + c + u] = q[u];
+            }
+        }
     };
 
     for (int64_t row = a + ln.j; row < a + n32; row += 32) {
@@ -437,7 +456,7 @@ __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
         if (row < a + L) {
             double pi[CPL], q[CPL];
             row_pq(row, pi, q);
-            if (any_live) {
+            if (!STOREQ && any_live) {
                 double *qs = qside + ((int64_t)ln.t * 32 + ln.j) * ld + c;
 #pragma unroll
                 for (int u = 0; u < CPL; ++u)
@@ -455,12 +474,13 @@ __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
 // Iteration t, kernel 2 (after alpha_t is known):
 //   q_t = L_reg p_t recomputed from the stored p_t (same fold, same bits),
 //   r_{t+1} = r_t - fl(alpha_t q_t); chains of dot(r_{t+1}, r_{t+1}).
-template <int CPL>
+template <int CPL, bool STOREQ>
 __global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
                                                 const int64_t *__restrict__ lp,
                                                 const int32_t *__restrict__ li,
                                                 const double *__restrict__ lv,
                                                 const double *__restrict__ P,
+                                                const double *__restrict__ Q,
                                                 double *__restrict__ R,
                                                 const double *__restrict__ alpha,
                                                 const int32_t *__restrict__ active,
@@ -484,10 +504,16 @@ __global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
 #pragma unroll
     for (int u = 0; u < CPL; ++u) s[u] = 0.0;
     auto upd = [&](int64_t row, Vec<CPL> &rv) {
-        const int64_t e0 = lp[row], e1 = lp[row + 1];
         double q[CPL];
 #pragma unroll
         for (int u = 0; u < CPL; ++u) q[u] = 0.0;
+        if (STOREQ) {
+            Vec<CPL> qv;
+            qv.load(Q + row * ld + c);
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) q[u] = qv.v[u];
+        }
+        const int64_t e0 = STOREQ ? 0 : lp[row], e1 = STOREQ ? 0 : lp[row + 1];
         for (int64_t e = e0; e < e1; ++e) {
             const int32_t col = li[e];
             const double w = lv[e];
@@ -526,6 +552,208 @@ __global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
 #pragma unroll
     for (int u = 0; u < CPL; ++u)
         if (live[u]) acc[((c + u - G.col0) * kMaxChunks + ln.t) * 32 + ln.j] = s[u];
+}
+
+// Split mode (rows with many entries, where recomputing a neighbour's p costs
+// two gathers): iteration t as three streaming/gathering kernels
+//   k_cg_p : x += fl(alpha_{t-1} p_{t-1}) (pending columns); p_t = fl(fl(beta p) + r)
+//   k_cg_q : q_t = L_reg p_t (gathers of the stored p), q stored; chains of dot(p, q)
+//   k_cg_upd<STOREQ>: r -= fl(alpha q) streaming q
+template <bool FIRST, int CPL>
+__global__ void __launch_bounds__(256) k_cg_p(CgGeom G, ChunkArg ch, const double *__restrict__ R,
+                                              const double *__restrict__ Pold,
+                                              double *__restrict__ Pnew, double *__restrict__ X,
+                                              const double *__restrict__ rho,
+                                              const double *__restrict__ rho_prev,
+                                              const double *__restrict__ alpha,
+                                              const int32_t *__restrict__ active,
+                                              const int32_t *__restrict__ xstep, int32_t it) {
+    const CgLane ln = cg_lane<CPL>(G);
+    if (!ln.ok) return;
+    const int64_t ld = G.ld, c = ln.c;
+    bool live[CPL], xp[CPL];
+    double beta[CPL], al[CPL];
+    bool any_live = false, any_x = false;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+        const bool in = (c + u) < G.col1;
+        live[u] = in && active[c + u];
+        xp[u] = !FIRST && in && xstep[c + u] == it - 1;
+        beta[u] = (!FIRST && live[u]) ? rho[c + u] / rho_prev[c + u] : 0.0;
+        al[u] = xp[u] ? alpha[c + u] : 0.0;
+        any_live = any_live || live[u];
+        any_x = any_x || xp[u];
+    }
+    if (!any_live && !any_x) return;
+    const int64_t a = ch.a[ln.t], L = ch.len[ln.t];
+    for (int64_t row = a + ln.j; row < a + L; row += 32) {
+        const int64_t o = row * ld + c;
+        Vec<CPL> po, rv;
+        if (!FIRST) po.load(Pold + o);
+        if (!FIRST && any_x) {
+            Vec<CPL> xv;
+            xv.load(X + o);
+#pragma unroll
+            for (int u = 0; u < CPL; ++u)
+                if (xp[u]) {
+                    double t1 = al[u] * po.v[u];
+                    xv.v[u] = xv.v[u] + t1;
+                }
+            xv.store(X + o);
+        }
+        if (!any_live) continue;
+        rv.load(R + o);
+        Vec<CPL> pw;
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            double pn;
+            if (FIRST) {
+                pn = rv.v[u];
+            } else {
+                double pb = po.v[u] * beta[u];
+                pn = pb + rv.v[u];
+            }
+            pw.v[u] = pn;
+        }
+        if (CPL == 1 || (live[0] && live[CPL - 1])) {
+            pw.store(Pnew + o);
+        } else {
+#pragma unroll
+            for (int u = 0; u < CPL; ++u)
+                if (live[u]) Pnew[o + u] = pw.v[u];
+        }
+    }
+}
+
+template <int CPL>
+__global__ void __launch_bounds__(256) k_cg_q(CgGeom G, ChunkArg ch, const int64_t *__restrict__ lp,
+                                              const int32_t *__restrict__ li,
+                                              const double *__restrict__ lv,
+                                              const double *__restrict__ P,
+                                              double *__restrict__ Q,
+                                              const int32_t *__restrict__ active,
+                                              double *__restrict__ acc) {
+    const CgLane ln = cg_lane<CPL>(G);
+    if (!ln.ok) return;
+    const int64_t ld = G.ld, c = ln.c;
+    bool live[CPL];
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+        live[u] = (c + u) < G.col1 && active[c + u];
+        any = any || live[u];
+    }
+    if (!any) return;
+    const int64_t a = ch.a[ln.t], L = ch.len[ln.t];
+    const int64_t n1 = L & ~(int64_t)15, n32 = n1 & ~(int64_t)31;
+    double s[CPL];
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) s[u] = 0.0;
+    auto row_q = [&](int64_t row, double *pi, double *q) {
+        const int64_t e0 = lp[row], e1 = lp[row + 1];
+        bool found = false;
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) q[u] = 0.0;
+        for (int64_t e = e0; e < e1; ++e) {
+            const int32_t col = li[e];
+            const double w = lv[e];
+            Vec<CPL> pv;
+            pv.load(P + col * ld + c);
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                if (col == row) pi[u] = pv.v[u];
+                double prod = w * pv.v[u];
+                q[u] = q[u] + prod;
+            }
+            found = found || (col == row);
+        }
+        if (!found) {  // L_reg_ii dropped (== 0): p_i still needed
+            Vec<CPL> pv;
+            pv.load(P + row * ld + c);
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) pi[u] = pv.v[u];
+        }
+        Vec<CPL> qw;
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) qw.v[u] = q[u];
+        if (CPL == 1 || (live[0] && live[CPL - 1])) {
+            qw.store(Q + row * ld + c);
+        } else {
+#pragma unroll
+            for (int u = 0; u < CPL; ++u)
+                if (live[u]) Q[row * ld + c + u] = q[u];
+        }
+    };
+    for (int64_t row = a + ln.j; row < a + n32; row += 32) {
+        double pi[CPL], q[CPL];
+        row_q(row, pi, q);
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) s[u] = __builtin_fma(pi[u], q[u], s[u]);
+    }
+    {
+        const int64_t row = a + n32 + ln.j;
+        if (row < a + L) {
+            double pi[CPL], q[CPL];
+            row_q(row, pi, q);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < CPL; ++u)
+        if (live[u]) acc[((c + u - G.col0) * kMaxChunks + ln.t) * 32 + ln.j] = s[u];
+}
+
+// q = L_reg p with no reduction attached, so any row order is allowed: waves
+// walk row tiles with the column block as the SLOWEST index, so the blocks in
+// flight (n x 64*CPL doubles each) stay resident in the Infinity Cache while
+// their rows are gathered.  dot(p, q) then comes from k_dot_acc.
+template <int CPL>
+__global__ void __launch_bounds__(256) k_spmv(CgGeom G, int64_t rpw, int64_t ntiles,
+                                              const int64_t *__restrict__ lp,
+                                              const int32_t *__restrict__ li,
+                                              const double *__restrict__ lv,
+                                              const double *__restrict__ P,
+                                              double *__restrict__ Q,
+                                              const int32_t *__restrict__ active) {
+    const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t cb = gw / ntiles, tile = gw % ntiles;
+    if (cb >= G.ncb) return;
+    const int64_t ld = G.ld, c = G.col0 + cb * (64 * CPL) + (int64_t)(threadIdx.x & 63) * CPL;
+    bool live[CPL];
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+        live[u] = (c + u) < G.col1 && active[c + u];
+        any = any || live[u];
+    }
+    if (!any) return;
+    const int64_t r0 = tile * rpw, r1 = r0 + rpw < G.n ? r0 + rpw : G.n;
+    for (int64_t row = r0; row < r1; ++row) {
+        const int64_t e0 = lp[row], e1 = lp[row + 1];
+        double q[CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) q[u] = 0.0;
+        for (int64_t e = e0; e < e1; ++e) {
+            const int32_t col = li[e];
+            const double w = lv[e];
+            Vec<CPL> pv;
+            pv.load(P + col * ld + c);
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                double prod = w * pv.v[u];
+                q[u] = q[u] + prod;
+            }
+        }
+        Vec<CPL> qw;
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) qw.v[u] = q[u];
+        if (CPL == 1 || (live[0] && live[CPL - 1])) {
+            qw.store(Q + row * ld + c);
+        } else {
+#pragma unroll
+            for (int u = 0; u < CPL; ++u)
+                if (live[u]) Q[row * ld + c + u] = q[u];
+        }
+    }
 }
 
 // after the loop: the x update of the last executed iteration
@@ -672,6 +900,7 @@ __global__ void __launch_bounds__(256) k_fin_pq(CgGeom G, const int64_t *__restr
                                                 const int64_t *__restrict__ cl, int count,
                                                 const double *__restrict__ acc,
                                                 const double *__restrict__ P,
+                                                const double *__restrict__ Qfull,
                                                 const double *__restrict__ qside,
                                                 const double *__restrict__ rho,
                                                 const int32_t *__restrict__ active, int32_t it,
@@ -680,7 +909,7 @@ __global__ void __launch_bounds__(256) k_fin_pq(CgGeom G, const int64_t *__restr
     const int64_t c = fin_column(G);
     if (c >= G.col1 || !active[c]) return;
     const double pq = ddot_finish_wave(acc + (c - G.col0) * kMaxChunks * 32, ca, cl, count, G.ld,
-                                       c, P, nullptr, qside);
+                                       c, P, Qfull, qside);
     if ((threadIdx.x & 63) != 0) return;
     alpha[c] = rho[c] / pq;
     xstep[c] = it;  // x += alpha p is applied by the next k_cg_pq (or the flush)
@@ -822,6 +1051,7 @@ int gs_er_prepare(gs_ctx *c, int64_t k, double reg, int64_t *m_out) {
         int64_t lnnz = 0;
         GS_HIP(hipMemcpyAsync(&lnnz, lp + n, 8, hipMemcpyDeviceToHost, c->stream));
         GS_HIP(hipStreamSynchronize(c->stream));
+        er.lnnz = lnnz;
         er.li.ensure(sizeof(int32_t) * (lnnz + 1));
         er.lv.ensure(sizeof(double) * (lnnz + 1));
         if (n)
@@ -899,8 +1129,26 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         G.npairs = G.ncb * ch.count;
         ColPtrs cp = col_ptrs(er);
         double *X = er.X.as<double>(), *Rr = er.Rr.as<double>();
-        // q of the < 32 leftover rows per chunk (the only q values the finish reads)
-        double *qside = (double *)er.Q.ensure(sizeof(double) * (size_t)ch.count * 32 * (size_t)er.ld);
+        // mode 0 (short rows, default): q recomputed in k_cg_upd from the stored p
+        // (one gather per entry is cheaper than 16 B/entry more of stream); only
+        // the q of the < 32 leftover rows per chunk is kept, for the finish.
+        // 1: q stored by the fused p/q kernel (GSPARSE_CG_STOREQ=1 selects it);
+        // 2: split p stream + SpMV on the stored p (long rows: one gather per entry
+        // instead of the fused kernel's two); 3: as 2 with the SpMV in
+        // column-block-major order (gathers served by the Infinity Cache) and a
+        // separate dot(p,q) pass -- the default for long rows.  GSPARSE_CG_MODE overrides.
+        int mode = (n > 0 && er.lnnz > kStoreQRowLen * n) ? 3 : 0;
+        if (const char *e = getenv("GSPARSE_CG_MODE")) {
+            const int v = atoi(e);
+            mode = (v >= 0 && v <= 3) ? v : 0;
+        }
+        if (const char *e = getenv("GSPARSE_CG_STOREQ")) mode = atoi(e) != 0 ? 1 : 0;
+        const bool storeq = mode != 0;
+        double *Qbuf = (double *)er.Q.ensure(
+            storeq ? sizeof(double) * (size_t)n * (size_t)er.ld
+                   : sizeof(double) * (size_t)ch.count * 32 * (size_t)er.ld);
+        double *qside = storeq ? nullptr : Qbuf;
+        double *Qfull = storeq ? Qbuf : nullptr;
         double *P[2] = {er.P0.as<double>(), er.P1.as<double>()};
         double *acc = er.acc.as<double>();
         // 8 workgroups (32 residues) per (column block, chunk) pair, XCD-grouped
@@ -915,9 +1163,10 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         auto *dch = (int64_t *)c->buf("er_chunks").ensure(sizeof(hch));
         GS_HIP(hipMemcpyAsync(dch, hch, sizeof(hch), hipMemcpyHostToDevice, c->stream));
         const int64_t *ca = dch, *cl = dch + kMaxChunks;
-        // algorithmic bytes: pq reads x, p, r and writes x, p (first iteration: r in, p out);
-        // upd reads p, r and writes r
-        const double bytes_pq = 40.0 * n * ncols, bytes_pq0 = 16.0 * n * ncols,
+        // algorithmic bytes: pq reads x, p, r and writes x, p (first iteration: r in, p out)
+        // (+ q written when stored); upd reads p (or q), r and writes r
+        const double qb = storeq ? 8.0 : 0.0;
+        const double bytes_pq = (40.0 + qb) * n * ncols, bytes_pq0 = (16.0 + qb) * n * ncols,
                      bytes_upd = 24.0 * n * ncols;
         const int64_t *lp = er.lp.as<int64_t>();
         const int32_t *li = er.li.as<int32_t>();
@@ -944,27 +1193,68 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             }
             double *Pold = P[cur], *Pnew = P[cur ^ 1];
             hipEvent_t t0 = prof_begin(c);
-#define GS_PQ(F, C)                                                                             \
-    k_cg_pq<F, C><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Rr, Pold, Pnew, X, qside,    \
-                                                cp.rho, cp.rho_prev, cp.alpha, cp.active, cp.xstep, \
-                                                it, acc)
-            if (it == 0) {
-                if (cpl == 2) GS_PQ(true, 2); else GS_PQ(true, 1);
+#define GS_PQ(F, C, S)                                                                        \
+    k_cg_pq<F, C, S><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Rr, Pold, Pnew, X, qside, \
+                                                   Qfull, cp.rho, cp.rho_prev, cp.alpha,        \
+                                                   cp.active, cp.xstep, it, acc)
+#define GS_PQ_S(F, C) \
+    if (storeq) GS_PQ(F, C, true); else GS_PQ(F, C, false)
+#define GS_P(F, C)                                                                          \
+    k_cg_p<F, C><<<grid, block, 0, c->stream>>>(G, ch, Rr, Pold, Pnew, X, cp.rho, cp.rho_prev, \
+                                               cp.alpha, cp.active, cp.xstep, it)
+#define GS_Q(C) k_cg_q<C><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Pnew, Qfull, cp.active, acc)
+            if (mode >= 2) {
+                if (it == 0) {
+                    if (cpl == 2) GS_P(true, 2); else GS_P(true, 1);
+                } else {
+                    if (cpl == 2) GS_P(false, 2); else GS_P(false, 1);
+                }
+                prof_end(c, t0, "cg_p", (it == 0 ? 16.0 : 40.0) * n * ncols);
+                t0 = prof_begin(c);
+                if (mode == 2) {
+                    if (cpl == 2) GS_Q(2); else GS_Q(1);
+                    prof_end(c, t0, "cg_q", 16.0 * n * ncols);
+                } else {
+                    // 4 rows per wave, 128 columns: best of {1..64} x {64, 128} on ogbn-arxiv size
+                    const int64_t rpw = 4;
+                    const int scpl = 2;
+                    CgGeom GS = G;
+                    GS.ncb = (int32_t)((ncols + 64 * scpl - 1) / (64 * scpl));
+                    const int64_t ntiles = (n + rpw - 1) / rpw;
+                    const unsigned sg = (unsigned)((GS.ncb * ntiles + 3) / 4);
+                    if (scpl == 2)
+                        k_spmv<2><<<sg, 256, 0, c->stream>>>(GS, rpw, ntiles, lp, li, lv, Pnew, Qfull, cp.active);
+                    else
+                        k_spmv<1><<<sg, 256, 0, c->stream>>>(GS, rpw, ntiles, lp, li, lv, Pnew, Qfull, cp.active);
+                    prof_end(c, t0, "cg_spmv", 8.0 * n * ncols);
+                    t0 = prof_begin(c);
+                    if (cpl == 2) k_dot_acc<2><<<grid, block, 0, c->stream>>>(G, ch, Pnew, Qfull, acc);
+                    else k_dot_acc<1><<<grid, block, 0, c->stream>>>(G, ch, Pnew, Qfull, acc);
+                    prof_end(c, t0, "cg_dot", 16.0 * n * ncols);
+                }
+            } else if (it == 0) {
+                if (cpl == 2) { GS_PQ_S(true, 2); } else { GS_PQ_S(true, 1); }
             } else {
-                if (cpl == 2) GS_PQ(false, 2); else GS_PQ(false, 1);
+                if (cpl == 2) { GS_PQ_S(false, 2); } else { GS_PQ_S(false, 1); }
             }
+#undef GS_P
+#undef GS_Q
+#undef GS_PQ_S
 #undef GS_PQ
-            prof_end(c, t0, "cg_pq", it == 0 ? bytes_pq0 : bytes_pq);
-            k_fin_pq<<<fgrid, 256, 0, c->stream>>>(G, ca, cl, ch.count, acc, Pnew, qside, cp.rho,
+            if (mode < 2) prof_end(c, t0, "cg_pq", it == 0 ? bytes_pq0 : bytes_pq);
+            k_fin_pq<<<fgrid, 256, 0, c->stream>>>(G, ca, cl, ch.count, acc, Pnew, Qfull, qside, cp.rho,
                                                    cp.active, it,
                                                   cp.alpha, cp.xstep);
             t0 = prof_begin(c);
-            if (cpl == 2)
-                k_cg_upd<2><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Pnew, Rr, cp.alpha,
-                                                           cp.active, acc);
-            else
-                k_cg_upd<1><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Pnew, Rr, cp.alpha,
-                                                           cp.active, acc);
+#define GS_UPD(C, S)                                                                     \
+    k_cg_upd<C, S><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Pnew, Qfull, Rr, cp.alpha, \
+                                                  cp.active, acc)
+            if (cpl == 2) {
+                if (storeq) GS_UPD(2, true); else GS_UPD(2, false);
+            } else {
+                if (storeq) GS_UPD(1, true); else GS_UPD(1, false);
+            }
+#undef GS_UPD
             prof_end(c, t0, "cg_upd", bytes_upd);
             k_fin_rr<<<fgrid, 256, 0, c->stream>>>(G, ca, cl, ch.count, acc, Rr, it, cp.rho,
                                                    cp.rho_prev, cp.atol,

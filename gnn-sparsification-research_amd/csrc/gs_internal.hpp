@@ -90,6 +90,7 @@ struct Graph {
 struct ErState {
     int64_t k = 0, m = 0, n = 0;
     int64_t ld = 0;         // row stride of the n x k arrays (k rounded up to 8)
+    int64_t lnnz = 0;       // entries of L_reg
     int64_t proj_next = 0;  // next R row expected by project_rows
     DevBuf edge_id;   // int64 [nnz] undirected edge id of CSR entry (u<v), -1 otherwise
     DevBuf bptr;      // int64 [n+1] incidence rows (B, metrics.py:260-269)

@@ -58,6 +58,17 @@ def test_approx_er_bit_exact(gs, name):
     assert bits_equal(er, ref), float(np.max(np.abs(er - ref) / np.abs(ref)))
 
 
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("name", ["karate_csr", "rmat10", "directed_dup", "roman2000"])
+def test_approx_er_all_cg_modes(gs, name, mode, monkeypatch):
+    """q recomputed in the update kernel (0), stored by the fused p/q kernel (1),
+    or split p stream + SpMV (2) -- the same bits in every mode."""
+    monkeypatch.setenv("GSPARSE_CG_MODE", mode)
+    g = load_golden(name)
+    sp_, _ = make(gs, g, with_x=False)
+    assert bits_equal(sp_._engine.approx_er(blas_threads=1), g["scores_approx_er"])
+
+
 def test_approx_er_roman_full_bit_exact(gs):
     """configs[1] size (n=22,662, E=65,854, k=2,674, 500 CG iterations per column)."""
     g = load_golden("roman_full")
