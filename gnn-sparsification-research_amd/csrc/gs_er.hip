@@ -325,7 +325,7 @@ struct Vec<2> {
 //   p_t = fl(fl(beta_t p_{t-1}) + r_t)  (own row stored; neighbours recomputed)
 //   q_t = L_reg p_t (per-row fold from 0.0, ascending column), kept only for the
 //         <32 leftover rows the ddot finish needs (qside); chains of dot(p_t, q_t).
-template <bool FIRST, int CPL, bool STOREQ>
+template <bool FIRST, int CPL, bool STOREQ, int RU>
 __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
                                                const int64_t *__restrict__ lp,
                                                const int32_t *__restrict__ li,
@@ -364,103 +364,163 @@ __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
 #pragma unroll
     for (int u = 0; u < CPL; ++u) s[u] = 0.0;
 
-    auto row_pq = [&](int64_t row, double *pi, double *q) {
+    // RU rows of the chain per trip (rows ok[i]; ok[0] always holds).  The trip
+    // is branch-free up to the stores: absent rows and entries past a row's
+    // end load from valid addresses (row[0], the row's last entry) and are
+    // masked by selects, so every load of a step is in flight at once.
+    auto rows_pq = [&](const int64_t *row, const bool *ok, double (*pi)[CPL], double (*q)[CPL]) {
+        int64_t rc[RU];
+#pragma unroll
+        for (int i = 0; i < RU; ++i) rc[i] = ok[i] ? row[i] : row[0];
+        Vec<CPL> po[RU], xv[RU];
         if (!FIRST && any_x) {
-            Vec<CPL> po, xv;
-            po.load(Pold + row * ld + c);
-            xv.load(X + row * ld + c);
 #pragma unroll
-            for (int u = 0; u < CPL; ++u)
-                if (xp[u]) {
-                    double t1 = al[u] * po.v[u];
-                    xv.v[u] = xv.v[u] + t1;
-                }
-            xv.store(X + row * ld + c);
+            for (int i = 0; i < RU; ++i) {
+                po[i].load(Pold + rc[i] * ld + c);
+                xv[i].load(X + rc[i] * ld + c);
+            }
         }
+        int64_t e0[RU], len[RU], maxlen = 0;
+        bool found[RU];
 #pragma unroll
-        for (int u = 0; u < CPL; ++u) {
-            q[u] = 0.0;
-            pi[u] = 0.0;
+        for (int i = 0; i < RU; ++i) {
+            e0[i] = lp[rc[i]];
+            len[i] = ok[i] ? lp[rc[i] + 1] - e0[i] : 0;
+            maxlen = len[i] > maxlen ? len[i] : maxlen;
+            found[i] = false;
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                q[i][u] = 0.0;
+                pi[i][u] = 0.0;
+            }
+        }
+        if (!any_live) maxlen = 0;
+        for (int64_t k = 0; k < maxlen; ++k) {
+            int32_t col[RU];
+            double w[RU];
+            Vec<CPL> rv[RU], pv[RU];
+#pragma unroll
+            for (int i = 0; i < RU; ++i) {
+                const int64_t kk = k < len[i] ? k : (len[i] > 0 ? len[i] - 1 : 0);
+                col[i] = li[e0[i] + kk];
+                w[i] = lv[e0[i] + kk];
+            }
+#pragma unroll
+            for (int i = 0; i < RU; ++i) {
+                rv[i].load(R + col[i] * ld + c);
+                if (!FIRST) pv[i].load(Pold + col[i] * ld + c);
+            }
+#pragma unroll
+            for (int i = 0; i < RU; ++i) {
+                const bool act = k < len[i];
+                const bool diag = act && col[i] == row[i];
+#pragma unroll
+                for (int u = 0; u < CPL; ++u) {
+                    double pn;
+                    if (FIRST) {
+                        pn = rv[i].v[u];
+                    } else {
+                        double pb = pv[i].v[u] * beta[u];
+                        pn = pb + rv[i].v[u];
+                    }
+                    pi[i][u] = diag ? pn : pi[i][u];
+                    double prod = w[i] * pn;
+                    double qn = q[i][u] + prod;
+                    q[i][u] = act ? qn : q[i][u];
+                }
+                found[i] = found[i] || diag;
+            }
+        }
+        if (!FIRST && any_x) {
+#pragma unroll
+            for (int i = 0; i < RU; ++i)
+                if (ok[i]) {
+#pragma unroll
+                    for (int u = 0; u < CPL; ++u)
+                        if (xp[u]) {
+                            double t1 = al[u] * po[i].v[u];
+                            xv[i].v[u] = xv[i].v[u] + t1;
+                        }
+                    xv[i].store(X + row[i] * ld + c);
+                }
         }
         if (!any_live) return;
-        const int64_t e0 = lp[row], e1 = lp[row + 1];
-        bool found = false;
-        for (int64_t e = e0; e < e1; ++e) {
-            const int32_t col = li[e];
-            const double w = lv[e];
-            Vec<CPL> rv, pv;
-            rv.load(R + col * ld + c);
-            if (!FIRST) pv.load(Pold + col * ld + c);
 #pragma unroll
-            for (int u = 0; u < CPL; ++u) {
-                double pn;
-                if (FIRST) {
-                    pn = rv.v[u];
-                } else {
-                    double pb = pv.v[u] * beta[u];
-                    pn = pb + rv.v[u];
-                }
-                if (col == row) pi[u] = pn;
-                double prod = w * pn;
-                q[u] = q[u] + prod;
-            }
-            found = found || (col == row);
-        }
-        if (!found) {  // L_reg_ii dropped (== 0): p_i still needed
-            Vec<CPL> rv, pv;
-            rv.load(R + row * ld + c);
-            if (!FIRST) pv.load(Pold + row * ld + c);
+        for (int i = 0; i < RU; ++i) {
+            if (!ok[i]) continue;
+            if (!found[i]) {  // L_reg_ii dropped (== 0): p_i still needed
+                Vec<CPL> rv, pv;
+                rv.load(R + row[i] * ld + c);
+                if (!FIRST) pv.load(Pold + row[i] * ld + c);
 #pragma unroll
-            for (int u = 0; u < CPL; ++u) {
-                if (FIRST) {
-                    pi[u] = rv.v[u];
-                } else {
-                    double pb = pv.v[u] * beta[u];
-                    pi[u] = pb + rv.v[u];
+                for (int u = 0; u < CPL; ++u) {
+                    if (FIRST) {
+                        pi[i][u] = rv.v[u];
+                    } else {
+                        double pb = pv.v[u] * beta[u];
+                        pi[i][u] = pb + rv.v[u];
+                    }
                 }
             }
-        }
-        Vec<CPL> pw;
+            const int64_t o = row[i] * ld + c;
+            Vec<CPL> pw;
 #pragma unroll
-        for (int u = 0; u < CPL; ++u) pw.v[u] = live[u] ? pi[u] : 0.0;
-        // columns that are not live keep their last p (the flush may need it)
-        if (CPL == 1 || (live[0] && live[CPL - 1])) {
-            pw.store(Pnew + row * ld + c);
-        } else {
-#pragma unroll
-            for (int u = 0; u < CPL; ++u)
-                if (live[u]) Pnew[row * ld + c + u] = pi[u];
-        }
-        if (STOREQ) {  // high-degree graphs: q kept, the update kernel streams it
-            Vec<CPL> qw;
-#pragma unroll
-            for (int u = 0; u < CPL; ++u) qw.v[u] = q[u];
+            for (int u = 0; u < CPL; ++u) pw.v[u] = live[u] ? pi[i][u] : 0.0;
+            // columns that are not live keep their last p (the flush may need it)
             if (CPL == 1 || (live[0] && live[CPL - 1])) {
-                qw.store(Q + row * ld + c);
+                pw.store(Pnew + o);
             } else {
 #pragma unroll
                 for (int u = 0; u < CPL; ++u)
-                    if (live[u]) Q[row * ld + c + u] = q[u];
+                    if (live[u]) Pnew[o + u] = pi[i][u];
+            }
+            if (STOREQ) {  // q kept, the update kernel streams it
+                Vec<CPL> qw;
+#pragma unroll
+                for (int u = 0; u < CPL; ++u) qw.v[u] = q[i][u];
+                if (CPL == 1 || (live[0] && live[CPL - 1])) {
+                    qw.store(Q + o);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < CPL; ++u)
+                        if (live[u]) Q[o + u] = q[i][u];
+                }
             }
         }
     };
 
-    for (int64_t row = a + ln.j; row < a + n32; row += 32) {
-        double pi[CPL], q[CPL];
-        row_pq(row, pi, q);
+    for (int64_t base = a + ln.j; base < a + n32; base += 32 * RU) {
+        int64_t row[RU];
+        bool ok[RU];
 #pragma unroll
-        for (int u = 0; u < CPL; ++u) s[u] = __builtin_fma(pi[u], q[u], s[u]);
+        for (int i = 0; i < RU; ++i) {
+            row[i] = base + 32 * i;
+            ok[i] = row[i] < a + n32;
+        }
+        double pi[RU][CPL], q[RU][CPL];
+        rows_pq(row, ok, pi, q);
+#pragma unroll
+        for (int i = 0; i < RU; ++i)
+            if (ok[i])
+#pragma unroll
+                for (int u = 0; u < CPL; ++u) s[u] = __builtin_fma(pi[i][u], q[i][u], s[u]);
     }
     {  // leftover rows of the chunk (16-block + tail): q kept for the finish
-        const int64_t row = a + n32 + ln.j;
-        if (row < a + L) {
-            double pi[CPL], q[CPL];
-            row_pq(row, pi, q);
+        int64_t row[RU];
+        bool ok[RU];
+#pragma unroll
+        for (int i = 0; i < RU; ++i) {
+            row[i] = a + n32 + ln.j;
+            ok[i] = i == 0 && row[i] < a + L;
+        }
+        if (ok[0]) {
+            double pi[RU][CPL], q[RU][CPL];
+            rows_pq(row, ok, pi, q);
             if (!STOREQ && any_live) {
                 double *qs = qside + ((int64_t)ln.t * 32 + ln.j) * ld + c;
 #pragma unroll
                 for (int u = 0; u < CPL; ++u)
-                    if (live[u]) qs[u] = q[u];
+                    if (live[u]) qs[u] = q[0][u];
             }
         }
     }
@@ -472,9 +532,9 @@ __global__ void __launch_bounds__(256) k_cg_pq(CgGeom G, ChunkArg ch,
 }
 
 // Iteration t, kernel 2 (after alpha_t is known):
-//   q_t = L_reg p_t recomputed from the stored p_t (same fold, same bits),
-//   r_{t+1} = r_t - fl(alpha_t q_t); chains of dot(r_{t+1}, r_{t+1}).
-template <int CPL, bool STOREQ>
+//   q_t = L_reg p_t recomputed from the stored p_t (same fold, same bits) or
+//   read (STOREQ), r_{t+1} = r_t - fl(alpha_t q_t); chains of dot(r_{t+1}, r_{t+1}).
+template <int CPL, bool STOREQ, int RU>
 __global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
                                                 const int64_t *__restrict__ lp,
                                                 const int32_t *__restrict__ li,
@@ -503,50 +563,84 @@ __global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
     double s[CPL];
 #pragma unroll
     for (int u = 0; u < CPL; ++u) s[u] = 0.0;
-    auto upd = [&](int64_t row, Vec<CPL> &rv) {
-        double q[CPL];
+    auto rows_upd = [&](const int64_t *row, const bool *ok, Vec<CPL> *rv) {
+        double q[RU][CPL];
+        int64_t rc[RU], e0[RU], len[RU], maxlen = 0;
 #pragma unroll
-        for (int u = 0; u < CPL; ++u) q[u] = 0.0;
-        if (STOREQ) {
-            Vec<CPL> qv;
-            qv.load(Q + row * ld + c);
+        for (int i = 0; i < RU; ++i) {
+            rc[i] = ok[i] ? row[i] : row[0];
+            rv[i].load(R + rc[i] * ld + c);
 #pragma unroll
-            for (int u = 0; u < CPL; ++u) q[u] = qv.v[u];
+            for (int u = 0; u < CPL; ++u) q[i][u] = 0.0;
+            if (STOREQ) {
+                Vec<CPL> qv;
+                qv.load(Q + rc[i] * ld + c);
+#pragma unroll
+                for (int u = 0; u < CPL; ++u) q[i][u] = qv.v[u];
+            }
+            e0[i] = STOREQ ? 0 : lp[rc[i]];
+            len[i] = (!STOREQ && ok[i]) ? lp[rc[i] + 1] - e0[i] : 0;
+            maxlen = len[i] > maxlen ? len[i] : maxlen;
         }
-        const int64_t e0 = STOREQ ? 0 : lp[row], e1 = STOREQ ? 0 : lp[row + 1];
-        for (int64_t e = e0; e < e1; ++e) {
-            const int32_t col = li[e];
-            const double w = lv[e];
-            Vec<CPL> pv;
-            pv.load(P + col * ld + c);
+        for (int64_t k = 0; k < maxlen; ++k) {
+            double w[RU];
+            Vec<CPL> pv[RU];
 #pragma unroll
-            for (int u = 0; u < CPL; ++u) {
-                double prod = w * pv.v[u];
-                q[u] = q[u] + prod;
+            for (int i = 0; i < RU; ++i) {
+                const int64_t kk = k < len[i] ? k : (len[i] > 0 ? len[i] - 1 : 0);
+                const int32_t col = li[e0[i] + kk];
+                w[i] = lv[e0[i] + kk];
+                pv[i].load(P + col * ld + c);
+            }
+#pragma unroll
+            for (int i = 0; i < RU; ++i) {
+                const bool act = k < len[i];
+#pragma unroll
+                for (int u = 0; u < CPL; ++u) {
+                    double prod = w[i] * pv[i].v[u];
+                    double qn = q[i][u] + prod;
+                    q[i][u] = act ? qn : q[i][u];
+                }
             }
         }
-        const int64_t o = row * ld + c;
-        rv.load(R + o);
 #pragma unroll
-        for (int u = 0; u < CPL; ++u) {
-            double t2 = al[u] * q[u];
-            rv.v[u] = live[u] ? rv.v[u] - t2 : rv.v[u];
-        }
-        rv.store(R + o);
+        for (int i = 0; i < RU; ++i)
+            if (ok[i]) {
+#pragma unroll
+                for (int u = 0; u < CPL; ++u) {
+                    double t2 = al[u] * q[i][u];
+                    rv[i].v[u] = live[u] ? rv[i].v[u] - t2 : rv[i].v[u];
+                }
+                rv[i].store(R + row[i] * ld + c);
+            }
     };
-    int64_t row = a + ln.j;
-    const int64_t end = a + n32;
-    for (; row < end; row += 32) {
-        Vec<CPL> r0;
-        upd(row, r0);
+    for (int64_t base = a + ln.j; base < a + n32; base += 32 * RU) {
+        int64_t row[RU];
+        bool ok[RU];
 #pragma unroll
-        for (int u = 0; u < CPL; ++u) s[u] = __builtin_fma(r0.v[u], r0.v[u], s[u]);
+        for (int i = 0; i < RU; ++i) {
+            row[i] = base + 32 * i;
+            ok[i] = row[i] < a + n32;
+        }
+        Vec<CPL> rv[RU];
+        rows_upd(row, ok, rv);
+#pragma unroll
+        for (int i = 0; i < RU; ++i)
+            if (ok[i])
+#pragma unroll
+                for (int u = 0; u < CPL; ++u) s[u] = __builtin_fma(rv[i].v[u], rv[i].v[u], s[u]);
     }
     {
-        const int64_t lrow = a + n32 + ln.j;
-        if (lrow < a + L) {
-            Vec<CPL> r0;
-            upd(lrow, r0);
+        int64_t row[RU];
+        bool ok[RU];
+#pragma unroll
+        for (int i = 0; i < RU; ++i) {
+            row[i] = a + n32 + ln.j;
+            ok[i] = i == 0 && row[i] < a + L;
+        }
+        if (ok[0]) {
+            Vec<CPL> rv[RU];
+            rows_upd(row, ok, rv);
         }
     }
 #pragma unroll
@@ -1118,7 +1212,8 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         // two columns per lane (16-B accesses) unless that leaves too few waves
         const int64_t ncols = col1 - col0;
         const int64_t waves2 = ((ncols + 127) / 128) * 32 * (int64_t)ch.count;
-        const int cpl = waves2 >= 4096 ? 2 : 1;
+        int cpl = waves2 >= 4096 ? 2 : 1;
+        if (const char *e = getenv("GSPARSE_CG_CPL")) cpl = atoi(e) == 1 ? 1 : 2;
         CgGeom G;
         G.n = n;
         G.k = k;
@@ -1144,6 +1239,14 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         }
         if (const char *e = getenv("GSPARSE_CG_STOREQ")) mode = atoi(e) != 0 ? 1 : 0;
         const bool storeq = mode != 0;
+        // chain rows per trip in the fused kernels (loads of all of them in flight)
+        // (fewer waves -> more rows per trip; measured on Roman at k/1 .. k/8 columns)
+        const int64_t cg_waves = (int64_t)G.ncb * ch.count * 32;
+        int ru = cg_waves >= 4096 ? 1 : cg_waves >= 2048 ? 2 : 4;
+        if (const char *e = getenv("GSPARSE_CG_RU")) {
+            const int v = atoi(e);
+            ru = (v == 1 || v == 2 || v == 4 || v == 8) ? v : ru;
+        }
         double *Qbuf = (double *)er.Q.ensure(
             storeq ? sizeof(double) * (size_t)n * (size_t)er.ld
                    : sizeof(double) * (size_t)ch.count * 32 * (size_t)er.ld);
@@ -1193,10 +1296,17 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             }
             double *Pold = P[cur], *Pnew = P[cur ^ 1];
             hipEvent_t t0 = prof_begin(c);
-#define GS_PQ(F, C, S)                                                                        \
-    k_cg_pq<F, C, S><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Rr, Pold, Pnew, X, qside, \
-                                                   Qfull, cp.rho, cp.rho_prev, cp.alpha,        \
-                                                   cp.active, cp.xstep, it, acc)
+#define GS_PQU(F, C, S, U)                                                                     \
+    k_cg_pq<F, C, S, U><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Rr, Pold, Pnew, X,     \
+                                                      qside, Qfull, cp.rho, cp.rho_prev,        \
+                                                      cp.alpha, cp.active, cp.xstep, it, acc)
+#define GS_PQ(F, C, S)                 \
+    do {                               \
+        if (ru == 1) GS_PQU(F, C, S, 1); \
+        else if (ru == 2) GS_PQU(F, C, S, 2); \
+        else if (ru == 4) GS_PQU(F, C, S, 4); \
+        else GS_PQU(F, C, S, 8);       \
+    } while (0)
 #define GS_PQ_S(F, C) \
     if (storeq) GS_PQ(F, C, true); else GS_PQ(F, C, false)
 #define GS_P(F, C)                                                                          \
@@ -1241,20 +1351,29 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
 #undef GS_Q
 #undef GS_PQ_S
 #undef GS_PQ
+#undef GS_PQU
             if (mode < 2) prof_end(c, t0, "cg_pq", it == 0 ? bytes_pq0 : bytes_pq);
             k_fin_pq<<<fgrid, 256, 0, c->stream>>>(G, ca, cl, ch.count, acc, Pnew, Qfull, qside, cp.rho,
                                                    cp.active, it,
                                                   cp.alpha, cp.xstep);
             t0 = prof_begin(c);
-#define GS_UPD(C, S)                                                                     \
-    k_cg_upd<C, S><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Pnew, Qfull, Rr, cp.alpha, \
-                                                  cp.active, acc)
+#define GS_UPDU(C, S, U)                                                                    \
+    k_cg_upd<C, S, U><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Pnew, Qfull, Rr,      \
+                                                     cp.alpha, cp.active, acc)
+#define GS_UPD(C, S)                  \
+    do {                              \
+        if (ru == 1) GS_UPDU(C, S, 1); \
+        else if (ru == 2) GS_UPDU(C, S, 2); \
+        else if (ru == 4) GS_UPDU(C, S, 4); \
+        else GS_UPDU(C, S, 8);        \
+    } while (0)
             if (cpl == 2) {
                 if (storeq) GS_UPD(2, true); else GS_UPD(2, false);
             } else {
                 if (storeq) GS_UPD(1, true); else GS_UPD(1, false);
             }
 #undef GS_UPD
+#undef GS_UPDU
             prof_end(c, t0, "cg_upd", bytes_upd);
             k_fin_rr<<<fgrid, 256, 0, c->stream>>>(G, ca, cl, ch.count, acc, Rr, it, cp.rho,
                                                    cp.rho_prev, cp.atol,
