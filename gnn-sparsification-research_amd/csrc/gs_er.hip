@@ -719,6 +719,79 @@ __global__ void __launch_bounds__(256) k_cg_p(CgGeom G, ChunkArg ch, const doubl
     }
 }
 
+// k_cg_p without a reduction, so it streams flat: threads own a column pair
+// (16 B, flags loaded once), blockIdx.y a band of kFlatRows rows, rows
+// walked in order -- each wave reads 1 KB contiguous per row.
+static constexpr int kFlatRows = 16;
+
+template <bool FIRST>
+__global__ void __launch_bounds__(256) k_cg_p_flat(CgGeom G, const double *__restrict__ R,
+                                                   const double *__restrict__ Pold,
+                                                   double *__restrict__ Pnew,
+                                                   double *__restrict__ X,
+                                                   const double *__restrict__ rho,
+                                                   const double *__restrict__ rho_prev,
+                                                   const double *__restrict__ alpha,
+                                                   const int32_t *__restrict__ active,
+                                                   const int32_t *__restrict__ xstep, int32_t it) {
+    const int64_t c = G.col0 + 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    if (c >= G.col1) return;
+    bool live[2], xp[2];
+    double beta[2], al[2];
+    bool any_live = false, any_x = false;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const bool in = (c + u) < G.col1;
+        live[u] = in && active[c + u];
+        xp[u] = !FIRST && in && xstep[c + u] == it - 1;
+        beta[u] = (!FIRST && live[u]) ? rho[c + u] / rho_prev[c + u] : 0.0;
+        al[u] = xp[u] ? alpha[c + u] : 0.0;
+        any_live = any_live || live[u];
+        any_x = any_x || xp[u];
+    }
+    if (!any_live && !any_x) return;
+    const int64_t r0 = (int64_t)blockIdx.y * kFlatRows;
+    const int64_t r1 = r0 + kFlatRows < G.n ? r0 + kFlatRows : G.n;
+    for (int64_t row = r0; row < r1; ++row) {
+        const int64_t o = row * G.ld + c;
+        Vec<2> po, rv, xv;
+        if (!FIRST) po.load(Pold + o);
+        if (any_x) xv.load(X + o);
+        if (any_live) rv.load(R + o);
+        if (any_x) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                if (xp[u]) {
+                    double t1 = al[u] * po.v[u];
+                    xv.v[u] = xv.v[u] + t1;
+                }
+            if (xp[0] && xp[1]) xv.store(X + o);
+            else
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    if (xp[u]) X[o + u] = xv.v[u];
+        }
+        if (!any_live) continue;
+        Vec<2> pw;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            double pn;
+            if (FIRST) {
+                pn = rv.v[u];
+            } else {
+                double pb = po.v[u] * beta[u];
+                pn = pb + rv.v[u];
+            }
+            pw.v[u] = pn;
+        }
+        if (live[0] && live[1]) pw.store(Pnew + o);
+        else
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                if (live[u]) Pnew[o + u] = pw.v[u];
+    }
+}
+
 template <int CPL>
 __global__ void __launch_bounds__(256) k_cg_q(CgGeom G, ChunkArg ch, const int64_t *__restrict__ lp,
                                               const int32_t *__restrict__ li,
@@ -866,7 +939,7 @@ __global__ void k_x_flush(CgGeom G, const double *__restrict__ P, const double *
 }
 
 // plain dot accumulation (||b||^2 before the first iteration)
-template <int CPL>
+template <int CPL, int RU>
 __global__ void __launch_bounds__(256) k_dot_acc(CgGeom G, ChunkArg ch,
                                                  const double *__restrict__ A,
                                                  const double *__restrict__ B,
@@ -879,12 +952,24 @@ __global__ void __launch_bounds__(256) k_dot_acc(CgGeom G, ChunkArg ch,
     double s[CPL];
 #pragma unroll
     for (int u = 0; u < CPL; ++u) s[u] = 0.0;
-    for (int64_t row = a + ln.j; row < a + n32; row += 32) {
-        Vec<CPL> av, bv;
-        av.load(A + row * ld + c);
-        bv.load(B + row * ld + c);
+    // RU chain rows per trip, loads first (absent rows re-read the first row)
+    for (int64_t base = a + ln.j; base < a + n32; base += 32 * RU) {
+        Vec<CPL> av[RU], bv[RU];
+        bool ok[RU];
 #pragma unroll
-        for (int u = 0; u < CPL; ++u) s[u] = __builtin_fma(av.v[u], bv.v[u], s[u]);
+        for (int i = 0; i < RU; ++i) {
+            ok[i] = base + 32 * i < a + n32;
+            const int64_t row = ok[i] ? base + 32 * i : base;
+            av[i].load(A + row * ld + c);
+            bv[i].load(B + row * ld + c);
+        }
+#pragma unroll
+        for (int i = 0; i < RU; ++i)
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                const double f = __builtin_fma(av[i].v[u], bv[i].v[u], s[u]);
+                s[u] = ok[i] ? f : s[u];
+            }
     }
 #pragma unroll
     for (int u = 0; u < CPL; ++u)
@@ -1232,7 +1317,13 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         // instead of the fused kernel's two); 3: as 2 with the SpMV in
         // column-block-major order (gathers served by the Infinity Cache) and a
         // separate dot(p,q) pass -- the default for long rows.  GSPARSE_CG_MODE overrides.
-        int mode = (n > 0 && er.lnnz > kStoreQRowLen * n) ? 3 : 0;
+        // Short rows: recompute (0) while the chains give enough waves; fewer
+        // columns (a rank's share on N GPUs) -> stored q (1), then the split
+        // kernels (3); measured on Roman at k/1, k/2, k/4, k/8 columns.
+        int mode = (n > 0 && er.lnnz > kStoreQRowLen * n) ? 3
+                   : ncols >= 2048                        ? 0
+                   : ncols >= 512                         ? 1
+                                                          : 3;
         if (const char *e = getenv("GSPARSE_CG_MODE")) {
             const int v = atoi(e);
             mode = (v >= 0 && v <= 3) ? v : 0;
@@ -1276,8 +1367,8 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         const double *lv = er.lv.as<double>();
         GS_HIP(hipMemsetAsync(cp.nactive, 0, sizeof(int32_t), c->stream));
         // ||b|| and rho_0 (r = b.copy())
-        if (cpl == 2) k_dot_acc<2><<<grid, block, 0, c->stream>>>(G, ch, Rr, Rr, acc);
-        else k_dot_acc<1><<<grid, block, 0, c->stream>>>(G, ch, Rr, Rr, acc);
+        if (cpl == 2) k_dot_acc<2, 4><<<grid, block, 0, c->stream>>>(G, ch, Rr, Rr, acc);
+        else k_dot_acc<1, 4><<<grid, block, 0, c->stream>>>(G, ch, Rr, Rr, acc);
         k_fin_init<<<fgrid, 256, 0, c->stream>>>(G, ca, cl, ch.count, acc, Rr, rtol, cp.bn,
                                                   cp.atol, cp.rho, cp.active, cp.iters, cp.xstep,
                                                   cp.nactive);
@@ -1313,12 +1404,25 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
     k_cg_p<F, C><<<grid, block, 0, c->stream>>>(G, ch, Rr, Pold, Pnew, X, cp.rho, cp.rho_prev, \
                                                cp.alpha, cp.active, cp.xstep, it)
 #define GS_Q(C) k_cg_q<C><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Pnew, Qfull, cp.active, acc)
-            if (mode >= 2) {
+            if (mode == 3) {
+                const dim3 pg((unsigned)(((ncols + 1) / 2 + 255) / 256),
+                              (unsigned)((n + kFlatRows - 1) / kFlatRows));
+                if (it == 0)
+                    k_cg_p_flat<true><<<pg, 256, 0, c->stream>>>(G, Rr, Pold, Pnew, X, cp.rho,
+                                                                 cp.rho_prev, cp.alpha, cp.active,
+                                                                 cp.xstep, it);
+                else
+                    k_cg_p_flat<false><<<pg, 256, 0, c->stream>>>(G, Rr, Pold, Pnew, X, cp.rho,
+                                                                  cp.rho_prev, cp.alpha, cp.active,
+                                                                  cp.xstep, it);
+            } else if (mode == 2) {
                 if (it == 0) {
                     if (cpl == 2) GS_P(true, 2); else GS_P(true, 1);
                 } else {
                     if (cpl == 2) GS_P(false, 2); else GS_P(false, 1);
                 }
+            }
+            if (mode >= 2) {
                 prof_end(c, t0, "cg_p", (it == 0 ? 16.0 : 40.0) * n * ncols);
                 t0 = prof_begin(c);
                 if (mode == 2) {
@@ -1338,8 +1442,8 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
                         k_spmv<1><<<sg, 256, 0, c->stream>>>(GS, rpw, ntiles, lp, li, lv, Pnew, Qfull, cp.active);
                     prof_end(c, t0, "cg_spmv", 8.0 * n * ncols);
                     t0 = prof_begin(c);
-                    if (cpl == 2) k_dot_acc<2><<<grid, block, 0, c->stream>>>(G, ch, Pnew, Qfull, acc);
-                    else k_dot_acc<1><<<grid, block, 0, c->stream>>>(G, ch, Pnew, Qfull, acc);
+                    if (cpl == 2) k_dot_acc<2, 4><<<grid, block, 0, c->stream>>>(G, ch, Pnew, Qfull, acc);
+                    else k_dot_acc<1, 4><<<grid, block, 0, c->stream>>>(G, ch, Pnew, Qfull, acc);
                     prof_end(c, t0, "cg_dot", 16.0 * n * ncols);
                 }
             } else if (it == 0) {
