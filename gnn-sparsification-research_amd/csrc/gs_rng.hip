@@ -169,8 +169,9 @@ extern "C" int gs_er_project_pcg64(gs_ctx *c, uint64_t state_hi, uint64_t state_
         const u128 inc = ((u128)inc_hi << 64) | inc_lo;
         double *raw = (double *)er.rawbuf.ensure(sizeof(double) * (size_t)need);
         hipEvent_t t0 = prof_begin(c);
-        // expected draws per normal ~1.0125; start with 2% headroom
-        int64_t draws = need + need / 50 + 4 * (int64_t)kZigBlock;
+        // NumPy's ziggurat consumes 1.022 draws per normal on average (measured,
+        // 2e6 normals); start with 4% headroom so one attempt suffices
+        int64_t draws = need + need / 25 + 4 * (int64_t)kZigBlock;
         for (int attempt = 0; attempt < 8; ++attempt) {
             int64_t nblk = (draws + kZigBlock - 1) / kZigBlock;
             ZigTables T;
