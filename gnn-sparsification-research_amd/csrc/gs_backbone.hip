@@ -16,6 +16,10 @@
 //      d > w and is kept whatever its exact distance.
 #include "gs_internal.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
 namespace gs {
 
 static int bits_for_bb(uint64_t v) {
@@ -25,6 +29,7 @@ static int bits_for_bb(uint64_t v) {
 }
 
 static constexpr uint64_t kInfBits = 0x7ff0000000000000ull;
+static constexpr int kBbLandmarkRounds = 256;  // frontier rounds per landmark search
 
 __global__ void k_bb_keys(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
                           const double *__restrict__ w, int64_t E, int64_t n,
@@ -143,6 +148,88 @@ struct BbSlab {
     int32_t *touched;          // n
 };
 
+// Bounded label-correcting search from u over G: dist[] (IEEE bits, +inf when
+// idle) holds the least fixpoint of d(y) = min_x fl(d(x) + w(x,y)) restricted
+// to values <= the bound s_wmax; touched[0 .. s_tcount) lists every node it
+// wrote.  After every frontier round the whole workgroup runs hook(), which
+// may lower s_wmax (never below a distance still needed) or end the search by
+// zeroing s_fcount; a node whose true distance is <= the final bound gets its
+// exact value, since no relaxation on its shortest path was ever cut.
+template <class Hook>
+__device__ void bb_search(const int64_t *__restrict__ gp, const int32_t *__restrict__ gi,
+                          const double *__restrict__ gw, int32_t u, const double &s_wmax,
+                          unsigned long long *__restrict__ dist, int32_t *__restrict__ qflag,
+                          int32_t *__restrict__ fa, int32_t *__restrict__ fb,
+                          int32_t *__restrict__ touched, int &s_fcount, int &s_ncount,
+                          int &s_tcount, unsigned long long &relax, Hook hook) {
+    if (threadIdx.x == 0) {
+        dist[u] = 0ull;  // +0.0
+        fa[0] = (int32_t)u;
+        touched[0] = (int32_t)u;
+    }
+    __syncthreads();
+    int32_t *cur = fa, *nxt = fb;
+    while (true) {
+        const int fc = s_fcount;
+        if (fc == 0) break;
+        const double wmax = s_wmax;
+        for (int f = threadIdx.x; f < fc; f += blockDim.x) qflag[cur[f]] = 0;
+        __syncthreads();
+        for (int f = threadIdx.x; f < fc; f += blockDim.x) {
+            const int32_t x = cur[f];
+            const double dx = __longlong_as_double(
+                (long long)__hip_atomic_load(&dist[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            for (int64_t e = gp[x]; e < gp[x + 1]; ++e) {
+                ++relax;
+                const double nd = dx + gw[e];
+                if (!(nd <= wmax)) continue;
+                const int32_t y = gi[e];
+                const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
+                const unsigned long long old = atomicMin(&dist[y], nb);
+                if (nb < old) {
+                    if (old == kInfBits) {
+                        int t = atomicAdd(&s_tcount, 1);
+                        touched[t] = y;
+                    }
+                    if (atomicExch(&qflag[y], 1) == 0) {
+                        int q = atomicAdd(&s_ncount, 1);
+                        nxt[q] = y;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            s_fcount = s_ncount;
+            s_ncount = 0;
+        }
+        int32_t *t = cur;
+        cur = nxt;
+        nxt = t;
+        __syncthreads();
+        hook();
+    }
+}
+
+// block-wide max of v (values >= -1) into *out, which holds -1 on entry;
+// ends with a barrier
+__device__ void bb_block_max(double v, double *out) {
+    for (int off = 32; off > 0; off >>= 1) {
+        double o = __shfl_down(v, off, 64);
+        v = o > v ? o : v;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        unsigned long long *p = (unsigned long long *)out;
+        unsigned long long old = *p;
+        while (__longlong_as_double(old) < v) {
+            unsigned long long prev = atomicCAS(p, old, (unsigned long long)__double_as_longlong(v));
+            if (prev == old) break;
+            old = prev;
+        }
+    }
+    __syncthreads();
+}
+
 __global__ void __launch_bounds__(256) k_bb_sssp(
     const int64_t *__restrict__ gp, const int32_t *__restrict__ gi, const double *__restrict__ gw,
     int64_t n, const int64_t *__restrict__ sources, int64_t nsrc, const int64_t *__restrict__ optr,
@@ -152,7 +239,7 @@ __global__ void __launch_bounds__(256) k_bb_sssp(
     int32_t *__restrict__ fr_all, int32_t *__restrict__ touched_all,
     unsigned long long *__restrict__ relax_total) {
     __shared__ int s_fcount, s_ncount, s_tcount;
-    __shared__ double s_wmax;
+    __shared__ double s_wmax, s_wnext;
     __shared__ unsigned long long s_relax;
     unsigned long long *dist = dist_all + (int64_t)blockIdx.x * n;
     int32_t *qflag = qflag_all + (int64_t)blockIdx.x * n;
@@ -177,72 +264,38 @@ __global__ void __launch_bounds__(256) k_bb_sssp(
             int64_t idx = order[j];
             if (state[idx] == 0 && w[idx] > lm) lm = w[idx];
         }
-        for (int off = 32; off > 0; off >>= 1) {
-            double o = __shfl_down(lm, off, 64);
-            lm = o > lm ? o : lm;
-        }
-        if ((threadIdx.x & 63) == 0) {
-            // block max through a CAS loop on the bits (values >= -1)
-            unsigned long long *p = (unsigned long long *)&s_wmax;
-            unsigned long long old = *p;
-            while (__longlong_as_double(old) < lm) {
-                unsigned long long prev =
-                    atomicCAS(p, old, (unsigned long long)__double_as_longlong(lm));
-                if (prev == old) break;
-                old = prev;
-            }
-        }
-        __syncthreads();
-        const double wmax = s_wmax;
-        if (wmax < 0.0) {
+        bb_block_max(lm, &s_wmax);
+        if (s_wmax < 0.0) {
             __syncthreads();
             continue;  // nothing unresolved for this source
         }
-        if (threadIdx.x == 0) {
-            dist[u] = 0ull;  // +0.0
-            fa[0] = (int32_t)u;
-            touched[0] = (int32_t)u;
-        }
-        __syncthreads();
-        int32_t *cur = fa, *nxt = fb;
-        while (true) {
-            const int fc = s_fcount;
-            if (fc == 0) break;
-            for (int f = threadIdx.x; f < fc; f += blockDim.x) qflag[cur[f]] = 0;
+        // after each round: a target whose current (upper-bound) distance
+        // already proves w > fl(d + eps) is pruned for good; the bound drops to
+        // the largest weight still undecided, and the search ends when none is
+        auto hook = [&]() {
+            if (threadIdx.x == 0) s_wnext = -1.0;
             __syncthreads();
-            for (int f = threadIdx.x; f < fc; f += blockDim.x) {
-                const int32_t x = cur[f];
-                const double dx = __longlong_as_double(
-                    (long long)__hip_atomic_load(&dist[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                for (int64_t e = gp[x]; e < gp[x + 1]; ++e) {
-                    ++relax;
-                    const double nd = dx + gw[e];
-                    if (!(nd <= wmax)) continue;
-                    const int32_t y = gi[e];
-                    const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
-                    const unsigned long long old = atomicMin(&dist[y], nb);
-                    if (nb < old) {
-                        if (old == kInfBits) {
-                            int t = atomicAdd(&s_tcount, 1);
-                            touched[t] = y;
-                        }
-                        if (atomicExch(&qflag[y], 1) == 0) {
-                            int q = atomicAdd(&s_ncount, 1);
-                            nxt[q] = y;
-                        }
-                    }
+            double m = -1.0;
+            for (int64_t j = c0 + threadIdx.x; j < c1; j += blockDim.x) {
+                const int64_t idx = order[j];
+                if (state[idx] != 0) continue;
+                const unsigned long long db =
+                    __hip_atomic_load(&dist[dst[idx]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (db != kInfBits && w[idx] > __longlong_as_double((long long)db) + eps) {
+                    state[idx] = 2;
+                    continue;
                 }
+                m = w[idx] > m ? w[idx] : m;
             }
-            __syncthreads();
+            bb_block_max(m, &s_wnext);
             if (threadIdx.x == 0) {
-                s_fcount = s_ncount;
-                s_ncount = 0;
+                s_wmax = s_wnext;
+                if (s_wnext < 0.0) s_fcount = 0;
             }
-            int32_t *t = cur;
-            cur = nxt;
-            nxt = t;
             __syncthreads();
-        }
+        };
+        bb_search(gp, gi, gw, (int32_t)u, s_wmax, dist, qflag, fa, fb, touched, s_fcount,
+                  s_ncount, s_tcount, relax, hook);
         // classify unresolved targets
         for (int64_t j = c0 + threadIdx.x; j < c1; j += blockDim.x) {
             int64_t idx = order[j];
@@ -266,6 +319,116 @@ __global__ void __launch_bounds__(256) k_bb_sssp(
     atomicAdd(&s_relax, relax);
     __syncthreads();
     if (threadIdx.x == 0) atomicAdd(relax_total, s_relax);
+}
+
+// Full searches from K landmarks: D[x*K + l] = d_fl(landmark l, x) (+inf if
+// unreachable).  One workgroup per landmark.
+__global__ void __launch_bounds__(256) k_bb_landmarks(
+    const int64_t *__restrict__ gp, const int32_t *__restrict__ gi, const double *__restrict__ gw,
+    int64_t n, const int32_t *__restrict__ lm, int K, int max_rounds, double *__restrict__ D,
+    int32_t *__restrict__ complete, unsigned long long *__restrict__ dist_all,
+    int32_t *__restrict__ qflag_all, int32_t *__restrict__ fr_all,
+    int32_t *__restrict__ touched_all) {
+    __shared__ int s_fcount, s_ncount, s_tcount, s_rounds, s_cut;
+    __shared__ double s_inf;
+    unsigned long long *dist = dist_all + (int64_t)blockIdx.x * n;
+    int32_t *qflag = qflag_all + (int64_t)blockIdx.x * n;
+    int32_t *fa = fr_all + (int64_t)blockIdx.x * 2 * n;
+    int32_t *fb = fa + n;
+    int32_t *touched = touched_all + (int64_t)blockIdx.x * n;
+    unsigned long long relax = 0;
+    for (int l = blockIdx.x; l < K; l += gridDim.x) {
+        if (threadIdx.x == 0) {
+            s_fcount = 1;
+            s_ncount = 0;
+            s_tcount = 1;
+            s_inf = __builtin_inf();
+            s_rounds = 0;
+            s_cut = 0;
+        }
+        __syncthreads();
+        // capped at max_rounds frontier rounds (long-diameter graphs): the
+        // distances are then upper bounds only -- complete[l] = 0
+        bb_search(gp, gi, gw, lm[l], s_inf, dist, qflag, fa, fb, touched, s_fcount, s_ncount,
+                  s_tcount, relax, [&] {
+                      if (threadIdx.x == 0 && ++s_rounds >= max_rounds && s_fcount > 0) {
+                          s_fcount = 0;
+                          s_cut = 1;
+                      }
+                      __syncthreads();
+                  });
+        if (threadIdx.x == 0) complete[l] = !s_cut;
+        const int tc = s_tcount;
+        for (int t = threadIdx.x; t < tc; t += blockDim.x) {
+            const int32_t y = touched[t];
+            D[(int64_t)y * K + l] = __longlong_as_double((long long)dist[y]);
+            dist[y] = kInfBits;
+            qflag[y] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+// Certificates for unresolved columns (state 0), each implying the exact
+// comparison w <= fl(d + eps) the reference makes (d = the fl left-fold
+// Dijkstra distance; fl sums of <= 2^31 terms are within 1e-9 relative of the
+// exact path sums, which the margins below absorb):
+//  * an endpoint of degree 1 in G whose only neighbour is the other one: every
+//    path starts or ends with that edge, so d = w_G(u,v) exactly;
+//  * landmark upper bound: the walk u -> l -> v has fold <= (D_l(u)+D_l(v))(1+m),
+//    so w > fl(that + eps) proves w > fl(d + eps): prune;
+//  * landmark lower bound: d >= |D_l(u)-D_l(v)| - m (D_l(u)+D_l(v)), so
+//    w <= that proves w <= d <= fl(d + eps): keep; D_l(u) finite with D_l(v)
+//    infinite (or the reverse) means u and v are disconnected: d = inf, keep.
+// m = max(1e-8, 8 n 2^-53) bounds the relative rounding of folds over simple
+// paths (< n terms each, two of them per walk).
+__global__ void k_bb_certify(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
+                             const double *__restrict__ w, int64_t E,
+                             const int64_t *__restrict__ gp, const int32_t *__restrict__ gi,
+                             const double *__restrict__ gw, const double *__restrict__ D,
+                             const int32_t *__restrict__ complete, int K, double eps, double m,
+                             uint8_t *__restrict__ state) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (state[i] != 0) continue;
+        const int64_t u = src[i], v = dst[i];
+        const double wi = w[i];
+        const int64_t du = gp[u + 1] - gp[u], dv = gp[v + 1] - gp[v];
+        if ((du == 1 && gi[gp[u]] == v) || (dv == 1 && gi[gp[v]] == u)) {
+            const double wg = du == 1 && gi[gp[u]] == v ? gw[gp[u]] : gw[gp[v]];
+            state[i] = (wi <= wg + eps) ? 1 : 2;  // d = fl(0 + w_G) = w_G
+            continue;
+        }
+        uint8_t st = 0;
+        for (int l = 0; l < K && !st; ++l) {
+            const double a = D[u * K + l], b = D[v * K + l];
+            const bool fa = a != __builtin_inf(), fb = b != __builtin_inf();
+            const bool exact = complete[l] != 0;  // else D holds upper bounds only
+            if (fa != fb) {
+                if (exact) st = 1;  // different components
+            } else if (fa) {
+                const double ub = (a + b) * (1.0 + m);
+                if (wi > ub + eps) {
+                    st = 2;
+                } else if (exact) {
+                    const double hi = a > b ? a : b, lo = a > b ? b : a;
+                    const double lb = (hi - lo) - m * (hi + lo);
+                    if (wi <= lb) st = 1;
+                }
+            }
+        }
+        state[i] = st;
+    }
+}
+
+__global__ void k_bb_count0(const uint8_t *__restrict__ state, int64_t E,
+                            unsigned long long *__restrict__ cnt) {
+    unsigned long long c = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x)
+        c += state[i] == 0;
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
 }
 
 __global__ void k_bb_fill_u64(unsigned long long *p, int64_t n, unsigned long long v) {
@@ -319,7 +482,7 @@ extern "C" int gs_metric_backbone(gs_ctx *c, int64_t n, int64_t E, const int64_t
 #define BB(name) DevBuf &b_##name = c->buf("bb_" #name)
         BB(src); BB(dst); BB(w); BB(keys); BB(idx); BB(ukeys); BB(uw); BB(pay); BB(gp); BB(gi);
         BB(gw); BB(okeys); BB(order); BB(optr); BB(state); BB(flag); BB(pos); BB(sources);
-        BB(dist); BB(qflag); BB(fr); BB(touched); BB(misc); BB(keep);
+        BB(dist); BB(qflag); BB(fr); BB(touched); BB(misc); BB(keep); BB(lm); BB(land); BB(lcomp);
 #undef BB
         const int64_t *dsrc =
             (const int64_t *)to_device(c, b_src, src, sizeof(int64_t) * E, loc);
@@ -375,6 +538,41 @@ extern "C" int gs_metric_backbone(gs_ctx *c, int64_t n, int64_t E, const int64_t
             uint8_t *state = (uint8_t *)b_state.ensure(E);
             k_bb_witness<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, dw, E, gp, gi, gw, eps,
                                                                state);
+            // landmark / degree-1 certificates (GSPARSE_BB_LANDMARKS = K, 0 = off)
+            int K = 16;
+            if (const char *e = getenv("GSPARSE_BB_LANDMARKS")) K = atoi(e) < 0 ? 0 : atoi(e);
+            if (K > n) K = (int)n;
+            if (K > 0) {
+                // landmarks: the K highest-degree nodes of G
+                std::vector<int64_t> hgp(n + 1);
+                GS_HIP(hipMemcpyAsync(hgp.data(), gp, 8 * (n + 1), hipMemcpyDeviceToHost, s));
+                GS_HIP(hipStreamSynchronize(s));
+                std::vector<int32_t> ids(n);
+                for (int64_t x = 0; x < n; ++x) ids[x] = (int32_t)x;
+                std::partial_sort(ids.begin(), ids.begin() + K, ids.end(), [&](int32_t p, int32_t q) {
+                    const int64_t dp = hgp[p + 1] - hgp[p], dq = hgp[q + 1] - hgp[q];
+                    return dp != dq ? dp > dq : p < q;
+                });
+                int32_t *dlm = (int32_t *)b_lm.ensure(4 * K);
+                GS_HIP(hipMemcpyAsync(dlm, ids.data(), 4 * K, hipMemcpyHostToDevice, s));
+                double *D = (double *)b_land.ensure(8 * (size_t)K * n);
+                k_bb_fill_u64<<<grid_for((int64_t)K * n, 256, 65536), 256, 0, s>>>(
+                    (unsigned long long *)D, (int64_t)K * n, kInfBits);
+                unsigned long long *ldist = (unsigned long long *)b_dist.ensure(8 * (size_t)K * n);
+                int32_t *lq = (int32_t *)b_qflag.ensure(4 * (size_t)K * n);
+                int32_t *lfr = (int32_t *)b_fr.ensure(8 * (size_t)K * n);
+                int32_t *ltouch = (int32_t *)b_touched.ensure(4 * (size_t)K * n);
+                k_bb_fill_u64<<<grid_for((int64_t)K * n, 256, 65536), 256, 0, s>>>(ldist, (int64_t)K * n,
+                                                                                   kInfBits);
+                GS_HIP(hipMemsetAsync(lq, 0, 4 * (size_t)K * n, s));
+                int32_t *lcomp = (int32_t *)b_lcomp.ensure(4 * K);
+                k_bb_landmarks<<<(unsigned)K, 256, 0, s>>>(gp, gi, gw, n, dlm, K, kBbLandmarkRounds, D,
+                                                           lcomp, ldist, lq, lfr, ltouch);
+                const double mrg = std::max(1e-8, 8.0 * (double)n * 0x1p-53);
+                k_bb_certify<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, dw, E, gp, gi, gw, D,
+                                                                   lcomp, K, eps, mrg, state);
+                GS_HIP(hipGetLastError());
+            }
             // sources needing a search
             int64_t *flag = (int64_t *)b_flag.ensure(8 * (n + 1));
             int64_t *pos = (int64_t *)b_pos.ensure(8 * (n + 1));
@@ -387,6 +585,14 @@ extern "C" int gs_metric_backbone(gs_ctx *c, int64_t n, int64_t E, const int64_t
             }
             GS_HIP(hipStreamSynchronize(s));
             int64_t nsrc = lastp + lastf;
+            if (getenv("GSPARSE_BB_DEBUG")) {
+                k_bb_count0<<<grid_for(E, 256, 4096), 256, 0, s>>>(state, E, misc + 3);
+                unsigned long long open = 0;
+                GS_HIP(hipMemcpyAsync(&open, misc + 3, 8, hipMemcpyDeviceToHost, s));
+                GS_HIP(hipStreamSynchronize(s));
+                fprintf(stderr, "[backbone] open before searches=%llu sources=%lld\n", open,
+                        (long long)nsrc);
+            }
             if (nsrc > 0) {
                 int64_t *sources = (int64_t *)b_sources.ensure(8 * nsrc);
                 k_bb_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(flag, pos, n, sources);

@@ -246,6 +246,31 @@ def test_backbone_rmat12_vs_oracle(gs):
     assert np.array_equal(st["keep_mask"], keep_ref)
 
 
+@pytest.mark.parametrize("graph", ["rmat14", "hub", "roman"])
+def test_backbone_certificates_match_plain_search(gs, graph, monkeypatch):
+    """Landmark / degree-1 certificates (default) vs the plain 2-hop witness +
+    bounded search (GSPARSE_BB_LANDMARKS=0, pinned to the oracle above)."""
+    from gsparse import graphs
+    from gsparse.metric_backbone import backbone_mask
+
+    if graph == "rmat14":
+        ei, n = graphs.rmat(14, 8, seed=3), 1 << 14
+    elif graph == "hub":
+        ei, n = _hub_graph()
+    else:
+        ei, n = graphs.roman_like(), 22662
+    ip, ix, _ = O.canonical_csr(ei, n)
+    rows = np.repeat(np.arange(n), np.diff(ip))
+    cost_csr = O.scores_to_cost(O.jaccard(ip, ix), "jaccard")
+    pos = np.searchsorted(rows.astype(np.int64) * n + ix, ei[0].astype(np.int64) * n + ei[1])
+    w = cost_csr[pos]
+    keep = backbone_mask(ei, n, w)
+    monkeypatch.setenv("GSPARSE_BB_LANDMARKS", "0")
+    keep0 = backbone_mask(ei, n, w)
+    assert np.array_equal(keep, keep0)
+    assert 0 < keep.sum() < len(keep)
+
+
 def test_featcos_1433_bow_vs_oracle(gs):
     from gsparse import graphs
 
