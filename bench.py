@@ -127,13 +127,141 @@ def cpu_baseline_jaccard(ei, n, threads, max_edges=2_000_000):
                       f"({t:.2f}s); OpenBLAS threads={threads}"}
 
 
+def cpu_baseline_backbone(ei, n, w, n_src=16, seed=0):
+    """The reference's algorithm (metric_backbone.py:86-111: NetworkX Dijkstra
+    from every node over the undirected u<v graph, then the per-column test) on
+    `n_src` sampled source rows, extrapolated by (#rows with columns)/n_src."""
+    import networkx as nx
+
+    ei = np.asarray(ei)
+    m = ei[0] < ei[1]
+    G = nx.Graph()
+    G.add_nodes_from(range(n))
+    for a, b, x in zip(ei[0][m].tolist(), ei[1][m].tolist(), np.asarray(w)[m].tolist()):
+        if G.has_edge(a, b):
+            if x < G[a][b]["weight"]:
+                G[a][b]["weight"] = x
+        else:
+            G.add_edge(a, b, weight=x)
+    rows = np.unique(ei[0])
+    rng = np.random.default_rng(seed)
+    sample = rng.choice(rows, min(n_src, len(rows)), replace=False)
+    t0 = time.perf_counter()
+    for u in sample.tolist():
+        nx.single_source_dijkstra_path_length(G, u, weight="weight")
+    t = time.perf_counter() - t0
+    total = t * len(rows) / len(sample)
+    return {"value": float(ei.shape[1] / total), "unit": "scored edges/s", "cores": 1,
+            "kind": "port",
+            "sample": f"NetworkX Dijkstra from {len(sample)} of {len(rows)} source rows "
+                      f"({t:.2f}s), extrapolated to all rows ({total:.0f}s)"}
+
+
+def bench_backbone(args, world, rank, local_rank, dev, dist):
+    """configs[4]: metric_backbone prune on R-MAT (default scale 18) or the
+    Roman-like graph; costs = _scores_to_cost(Jaccard) as
+    sparsify_metric_backbone passes them (core.py:251-279).  One step = the
+    whole prune (graph build, witnesses, certificates, bounded searches) on
+    device-resident columns; N > 1 splits the source rows (u % N) and
+    all-reduces the keep bytes."""
+    import ctypes
+
+    from gsparse import graphs
+    from gsparse._lib import GS_DEVICE, Context
+    from gsparse.core import GraphSparsifier
+    from gsparse.data import Data
+    from gsparse.distributed import Comm
+
+    t_gen = time.perf_counter()
+    if args.bb_graph == "roman":
+        ei, n = graphs.roman_like(), 22_662
+        wl = "configs[4] metric backbone, Roman-like, Jaccard costs"
+    else:
+        ei, n = graphs.rmat(args.bb_scale, 8, seed=0), 1 << args.bb_scale
+        wl = f"configs[4] metric backbone, RMAT-{args.bb_scale}, Jaccard costs"
+    t_gen = time.perf_counter() - t_gen
+    E = ei.shape[1]
+    sp_ = GraphSparsifier(Data(edge_index=torch.from_numpy(ei), num_nodes=n), f"cuda:{local_rank}")
+    cost = sp_._scores_to_cost(sp_.compute_scores("jaccard"), "jaccard")[:E]
+    ctx = Context(local_rank)
+    src = torch.from_numpy(np.ascontiguousarray(ei[0])).to(dev)
+    dst = torch.from_numpy(np.ascontiguousarray(ei[1])).to(dev)
+    w = torch.from_numpy(np.ascontiguousarray(cost, dtype=np.float64)).to(dev)
+    keep = torch.empty(E, dtype=torch.uint8, device=dev)
+    comm = Comm(device=dev) if world > 1 else None
+    relax = ctypes.c_int64(0)
+
+    def step():
+        ctx.call("gs_metric_backbone_part", n, E, src.data_ptr(), dst.data_ptr(), w.data_ptr(),
+                 GS_DEVICE, 1e-9, rank, world, keep.data_ptr(), GS_DEVICE, ctypes.byref(relax))
+        if comm is not None:
+            return comm.all_reduce_sum(keep.to(torch.int32))
+        return keep
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ctx.profile(True)
+    ctx.profile_reset()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        if dist.get_backend() != "nccl":
+            t = t.cpu()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kept = int((out != 0).sum().item())
+    roofline = None
+    if prof and "metric_backbone" in prof:
+        p = prof["metric_backbone"]
+        avg_ms = p["ms"] / p["launches"]
+        bytes_per = p["bytes"] / p["launches"]
+        achieved = bytes_per / (avg_ms * 1e-3) / 1e9
+        roofline = {"kernel": "metric_backbone", "bound": "hbm", "achieved": round(achieved, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "avg_launch_ms": round(avg_ms, 3), "algorithmic_bytes_per_launch": bytes_per,
+                    "launches": p["launches"], "relaxations_per_launch_rank0": relax.value}
+    result = {
+        "metric": "scored edges/sec (metric backbone)", "value": round(E * args.steps / elapsed, 1),
+        "unit": "scored edges/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 2), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (stand-in graph of the config's size; datasets are not downloadable here)",
+        "config": {"workload": wl, "n": n, "E": E, "kept": kept,
+                   "parallelism": f"source-rows/{world}" if world > 1 else "1 GPU",
+                   "graph_gen_s": round(t_gen, 2)},
+        "roofline": roofline,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_backbone(ei, n, cost)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="roman", choices=["roman", "rmat", "arxiv"])
+    ap.add_argument("--workload", default="roman", choices=["roman", "rmat", "arxiv", "backbone"])
     ap.add_argument("--scale", type=int, default=22, help="R-MAT scale for --workload rmat")
+    ap.add_argument("--bb-graph", default="rmat", choices=["rmat", "roman"],
+                    help="graph of --workload backbone (R-MAT at --bb-scale, or Roman-like)")
+    ap.add_argument("--bb-scale", type=int, default=18)
     ap.add_argument("--blas-threads", type=int, default=8,
                     help="OpenBLAS ddot order to reproduce (reference run with this many threads)")
     ap.add_argument("--rng", default=os.environ.get("GSPARSE_ER_RNG", "device"),
@@ -162,6 +290,9 @@ def main():
     from gsparse._lib import Context
     from gsparse.distributed import Comm, sharded_approx_er, sharded_edge_scores
     from gsparse.engine import Engine, jl_dim
+
+    if args.workload == "backbone":
+        return bench_backbone(args, world, rank, local_rank, dev, dist)
 
     t_gen = time.perf_counter()
     if args.workload == "roman":

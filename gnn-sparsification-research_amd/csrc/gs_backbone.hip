@@ -437,12 +437,17 @@ __global__ void k_bb_fill_u64(unsigned long long *p, int64_t n, unsigned long lo
         p[i] = v;
 }
 
-// sources: rows with at least one unresolved target
+// sources: rows of this part (u % nparts == part) with an unresolved target
 __global__ void k_bb_need(const int64_t *__restrict__ optr, const int64_t *__restrict__ order,
-                          const uint8_t *__restrict__ state, int64_t n, int64_t *__restrict__ flag) {
+                          const uint8_t *__restrict__ state, int64_t n, int part, int nparts,
+                          int64_t *__restrict__ flag) {
     for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
          u += (int64_t)gridDim.x * blockDim.x) {
         int64_t f = 0;
+        if (u % nparts != part) {
+            flag[u] = 0;
+            continue;
+        }
         for (int64_t j = optr[u]; j < optr[u + 1]; ++j)
             if (state[order[j]] == 0) {
                 f = 1;
@@ -459,21 +464,26 @@ __global__ void k_bb_compact(const int64_t *__restrict__ flag, const int64_t *__
         if (flag[u]) sources[pos[u]] = u;
 }
 
-__global__ void k_bb_keep(const uint8_t *__restrict__ state, int64_t E, uint8_t *__restrict__ keep) {
+// keep bytes of this part's columns (source row u % nparts == part), 0 elsewhere
+__global__ void k_bb_keep(const uint8_t *__restrict__ state, const int64_t *__restrict__ src,
+                          int64_t E, int part, int nparts, uint8_t *__restrict__ keep) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
          i += (int64_t)gridDim.x * blockDim.x)
-        keep[i] = state[i] == 1;
+        keep[i] = state[i] == 1 && src[i] % nparts == part;
 }
 
 }  // namespace gs
 
 using namespace gs;
 
-extern "C" int gs_metric_backbone(gs_ctx *c, int64_t n, int64_t E, const int64_t *src,
-                                  const int64_t *dst, const double *w, int loc, double eps,
-                                  uint8_t *keep, int keep_loc, int64_t *n_relax) {
+extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const int64_t *src,
+                                       const int64_t *dst, const double *w, int loc, double eps,
+                                       int part, int nparts, uint8_t *keep, int keep_loc,
+                                       int64_t *n_relax) {
     return guard([&] {
         GS_CHECK(c, GS_EINVAL, "null context");
+        GS_CHECK(nparts >= 1 && 0 <= part && part < nparts, GS_EINVAL, "bad part %d of %d", part,
+                 nparts);
         GS_CHECK(n >= 0 && E >= 0, GS_EINVAL, "negative n/E");
         GS_CHECK(n < (int64_t(1) << 31), GS_EUNSUPPORTED, "n >= 2^31");
         GS_HIP(hipSetDevice(c->device));
@@ -576,7 +586,8 @@ extern "C" int gs_metric_backbone(gs_ctx *c, int64_t n, int64_t E, const int64_t
             // sources needing a search
             int64_t *flag = (int64_t *)b_flag.ensure(8 * (n + 1));
             int64_t *pos = (int64_t *)b_pos.ensure(8 * (n + 1));
-            k_bb_need<<<grid_for(n, 256, 8192), 256, 0, s>>>(optr, order, state, n, flag);
+            k_bb_need<<<grid_for(n, 256, 8192), 256, 0, s>>>(optr, order, state, n, part, nparts,
+                                                             flag);
             exclusive_scan_i64(c, flag, pos, n);
             int64_t lastp = 0, lastf = 0;
             if (n) {
@@ -613,7 +624,7 @@ extern "C" int gs_metric_backbone(gs_ctx *c, int64_t n, int64_t E, const int64_t
                                                           touched, misc + 1);
                 GS_HIP(hipGetLastError());
             }
-            k_bb_keep<<<grid_for(E, 256, 8192), 256, 0, s>>>(state, E, dkeep);
+            k_bb_keep<<<grid_for(E, 256, 8192), 256, 0, s>>>(state, dsrc, E, part, nparts, dkeep);
             unsigned long long hr = 0;
             GS_HIP(hipMemcpyAsync(&hr, misc + 1, 8, hipMemcpyDeviceToHost, s));
             GS_HIP(hipStreamSynchronize(s));
@@ -623,4 +634,10 @@ extern "C" int gs_metric_backbone(gs_ctx *c, int64_t n, int64_t E, const int64_t
         finish_out(c, keep, dkeep, E, keep_loc);
         if (n_relax) *n_relax = relax;
     });
+}
+
+extern "C" int gs_metric_backbone(gs_ctx *c, int64_t n, int64_t E, const int64_t *src,
+                                  const int64_t *dst, const double *w, int loc, double eps,
+                                  uint8_t *keep, int keep_loc, int64_t *n_relax) {
+    return gs_metric_backbone_part(c, n, E, src, dst, w, loc, eps, 0, 1, keep, keep_loc, n_relax);
 }

@@ -60,6 +60,8 @@ SIGNATURES = {
                             ctypes.POINTER(_f64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "gs_metric_backbone": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _int, _f64, _vp, _int,
                                   ctypes.POINTER(_i64)]),
+    "gs_metric_backbone_part": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _int, _f64, _int, _int,
+                                       _vp, _int, ctypes.POINTER(_i64)]),
 }
 
 

@@ -5,6 +5,8 @@ SURVEY §8(e):
     pair tasks (gs_jaccard_part: both CSR entries of a pair, zeros elsewhere)
     and one all-reduce(sum) assembles the whole vector -- exact, since every
     entry has exactly one non-zero contributor.
+  * metric backbone: the per-source searches by source row (u % world), one
+    all-reduce(sum) of the keep bytes.
   * AA / degree / FeatCos (and Jaccard on explicit ranges): contiguous CSR
     edge ranges (equal counts, or equal per-edge work d_u + d_v for skewed
     graphs), then an all-gather of the fp64 scores so every rank can run the
@@ -129,6 +131,19 @@ def sharded_edge_scores(engine, comm: Comm, metric: str, bounds: list[int] | Non
         raise ValueError(metric)
     sizes = [b[r + 1] - b[r] for r in range(comm.world)]
     return comm.all_gather_padded(comm.tensor(local), sizes)
+
+
+def sharded_backbone(comm: Comm, edge_index: np.ndarray, num_nodes: int,
+                     edge_weights: np.ndarray, epsilon: float = 1e-9, mask_fn=None) -> np.ndarray:
+    """metric_backbone keep mask with the per-source searches split over ranks
+    (source row u goes to rank u % world); one all-reduce(sum) of the keep
+    bytes -- each column is decided by exactly one rank."""
+    if mask_fn is None:
+        from .metric_backbone import backbone_mask as mask_fn
+    part = mask_fn(edge_index, num_nodes, edge_weights, epsilon, part=comm.rank,
+                   nparts=comm.world)
+    t = comm.tensor(np.ascontiguousarray(part, dtype=np.uint8).astype(np.int32))
+    return comm.all_reduce_sum(t).cpu().numpy().astype(bool)
 
 
 def sharded_approx_er(engine, comm: Comm, epsilon: float = 0.3, seed: int = 42,

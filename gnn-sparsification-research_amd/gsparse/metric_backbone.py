@@ -11,6 +11,7 @@ the same distances bit for bit, no APSP table.
 
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, Tuple
 
 import numpy as np
@@ -34,18 +35,21 @@ def _context(ctx: Context | None) -> Context:
 
 def backbone_mask(edge_index: np.ndarray, num_nodes: int, edge_weights: np.ndarray,
                   epsilon: float = 1e-9, ctx: Context | None = None,
-                  return_relax: bool = False):
-    """Keep mask (bool[E]) of the metric backbone; device computation."""
+                  return_relax: bool = False, part: int = 0, nparts: int = 1):
+    """Keep mask (bool[E]) of the metric backbone; device computation.
+
+    With nparts > 1 only the columns whose source row u has u % nparts == part
+    are decided here (the rest read False): the parts OR to the whole mask."""
     ei = np.asarray(edge_index, dtype=np.int64)
     E = ei.shape[1]
     src = np.ascontiguousarray(ei[0])
     dst = np.ascontiguousarray(ei[1])
     w = np.ascontiguousarray(np.asarray(edge_weights, dtype=np.float64)[:E])
     keep = np.zeros(max(E, 1), dtype=np.uint8)
-    relax = __import__("ctypes").c_int64(0)
+    relax = ctypes.c_int64(0)
     c = _context(ctx)
-    c.call("gs_metric_backbone", int(num_nodes), E, ptr(src), ptr(dst), ptr(w), GS_HOST,
-           float(epsilon), ptr(keep), GS_HOST, __import__("ctypes").byref(relax))
+    c.call("gs_metric_backbone_part", int(num_nodes), E, ptr(src), ptr(dst), ptr(w), GS_HOST,
+           float(epsilon), int(part), int(nparts), ptr(keep), GS_HOST, ctypes.byref(relax))
     mask = keep[:E].view(bool)
     return (mask, relax.value) if return_relax else mask
 

@@ -146,6 +146,13 @@ int gs_topk_mask(gs_ctx *ctx, const double *scores, int s_loc, int64_t nnz, int6
 int gs_metric_backbone(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src,
                        const int64_t *dst, const double *w, int loc, double eps,
                        uint8_t *keep, int keep_loc, int64_t *n_relax);
+/* Part `part` of `nparts` of gs_metric_backbone (multi-GPU): keep
+ * bytes of the columns whose source row u has u % nparts == part (their
+ * searches run here), 0 elsewhere -- the element-wise sum over parts equals
+ * the whole keep mask. */
+int gs_metric_backbone_part(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src,
+                            const int64_t *dst, const double *w, int loc, double eps, int part,
+                            int nparts, uint8_t *keep, int keep_loc, int64_t *n_relax);
 
 #ifdef __cplusplus
 }

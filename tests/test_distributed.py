@@ -85,8 +85,18 @@ def _worker(rank, world, port, name, q):
         jac_w = sharded_edge_scores(eng, comm, "jaccard",
                                     bounds=work_ranges(g["indptr"], g["indices"], world)).numpy()
         er = sharded_approx_er(eng, comm, blas_threads=1).numpy()
+        bb = None
+        if "backbone_jaccard" in g:
+            from gsparse.distributed import sharded_backbone
+
+            def oracle_part(ei, n, w, eps, part=0, nparts=1):
+                full = O.metric_backbone(ei, n, w, eps)
+                return full & ((ei[0] % nparts) == part)
+
+            bb = sharded_backbone(comm, g["edge_index"], int(g["num_nodes"]), g["cost_jaccard"],
+                                  mask_fn=oracle_part)
         if rank == 0:
-            q.put((jac, jac_w, er))
+            q.put((jac, jac_w, er, bb))
     finally:
         dist.destroy_process_group()
 
@@ -100,7 +110,7 @@ def test_sharded_equals_single(name, world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, name, q)) for r in range(world)]
     for p in procs:
         p.start()
-    jac, jac_w, er = q.get(timeout=600)
+    jac, jac_w, er, bb = q.get(timeout=600)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -108,6 +118,8 @@ def test_sharded_equals_single(name, world):
     assert np.array_equal(jac.view(np.uint64), g["scores_jaccard"].view(np.uint64))
     assert np.array_equal(jac_w.view(np.uint64), g["scores_jaccard"].view(np.uint64))
     assert np.array_equal(er.view(np.uint64), g["scores_approx_er"].view(np.uint64))
+    if bb is not None:
+        assert np.array_equal(bb, g["backbone_jaccard"])
 
 
 def test_tree_helpers():

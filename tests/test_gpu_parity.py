@@ -271,6 +271,23 @@ def test_backbone_certificates_match_plain_search(gs, graph, monkeypatch):
     assert 0 < keep.sum() < len(keep)
 
 
+@pytest.mark.parametrize("nparts", [2, 3, 4])
+def test_backbone_parts_sum_to_whole(gs, nparts):
+    from gsparse import graphs
+    from gsparse.metric_backbone import backbone_mask
+
+    ei, n = graphs.rmat(14, 8, seed=4), 1 << 14
+    ip, ix, _ = O.canonical_csr(ei, n)
+    w = O.scores_to_cost(O.jaccard(ip, ix), "jaccard")[: ei.shape[1]]
+    whole = backbone_mask(ei, n, w)
+    parts = [backbone_mask(ei, n, w, part=p, nparts=nparts) for p in range(nparts)]
+    tot = np.zeros(len(whole), dtype=int)
+    for p in parts:
+        tot += p
+    assert tot.max() <= 1
+    assert np.array_equal(tot.astype(bool), whole)
+
+
 def test_featcos_1433_bow_vs_oracle(gs):
     from gsparse import graphs
 
