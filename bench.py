@@ -41,6 +41,42 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+# profiler name -> kernel symbol prefix in the rocprofv3 summaries; "jaccard"
+# is a pipeline of kernels (plan, light, hash classes, bitmap), summed per call
+PMC_KERNEL = {"cg_pq": "gs::k_cg_pq<false", "cg_upd": "gs::k_cg_upd<", "jaccard": "gs::k_jac_",
+              "cg_p": "gs::k_cg_p", "cg_spmv": "gs::k_spmv<"}
+
+
+def pmc_traffic(name: str, workload: str):
+    """HBM bytes per launch of the dominant kernel from the newest committed
+    rocprofv3 --pmc summary of this workload (profiles/*_<workload>_pmc_summary.json,
+    made by tools/profile_bench.sh: separate FETCH_SIZE / WRITE_SIZE passes).
+    FETCH_SIZE counts 1/2 of a wide coalesced stream on gfx950 and is doubled,
+    WRITE_SIZE is exact (MI355X_MICROARCH.md, HBM section); both are KB."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_pmc_summary.json")))
+    pre = PMC_KERNEL.get(name)
+    if not files or pre is None:
+        return None, None
+    with open(files[-1]) as fh:
+        summ = json.load(fh)
+    hits = [(k, v) for k, v in summ.items() if k.startswith("void " + pre) or k.startswith(pre)]
+    hits = [(k, v) for k, v in hits if "FETCH_SIZE_KB_per_launch" in v and "WRITE_SIZE_KB_per_launch" in v]
+    if not hits:
+        return None, None
+    def kb(v):
+        return (2.0 * v["FETCH_SIZE_KB_per_launch"] + v["WRITE_SIZE_KB_per_launch"]) * 1024.0
+
+    if name == "jaccard":
+        calls = max(1, max(v.get("launches", 1) for k, v in hits if "k_jac_plan" in k) if any(
+            "k_jac_plan" in k for k, _ in hits) else 1)
+        b = sum(kb(v) * v.get("launches", 1) for _, v in hits) / calls
+        return b, f"{os.path.basename(files[-1])}: sum of {len(hits)} gs::k_jac_* kernels"
+    k, v = max(hits, key=lambda kv: kv[1].get("launches", 0))
+    return kb(v), f"{os.path.basename(files[-1])}: {k}"
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -373,11 +409,15 @@ def main():
         avg_ms = p["ms"] / p["launches"]
         bytes_per = p["bytes"] / p["launches"]
         achieved = bytes_per / (avg_ms * 1e-3) / 1e9
+        traffic, tsrc = pmc_traffic(name, args.workload)
         roofline = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": round(traffic) if traffic else None,
                     "avg_launch_ms": round(avg_ms, 5),
                     "algorithmic_bytes_per_launch": bytes_per, "launches": p["launches"]}
+        if tsrc:
+            roofline["traffic_source"] = tsrc
     kernels = {k2: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k2, v in prof.items()}
 
     result = {
