@@ -12,7 +12,7 @@
 //             recomputed; q = L_reg p (per-row fold from 0.0 in ascending
 //             column, products rounded); partial dot(p,q)
 //   k_cg_upd: q recomputed from the stored p; r -= fl(alpha q); partial dot(r,r)
-// (64 B per entry and iteration).  Long rows (mode 3): k_cg_p (p stream),
+// (64 B per entry and iteration).  Long rows (mode 3): k_cg_p_flat (p stream),
 // k_spmv (column-block-major SpMV, q stored), k_dot_acc, k_cg_upd<STOREQ>.
 // Plus two per-column finish kernels.  Every dot product reproduces
 // OpenBLAS ddot (SkylakeX kernel) as np.dot calls it: T thread chunks for
@@ -648,78 +648,13 @@ __global__ void __launch_bounds__(256) k_cg_upd(CgGeom G, ChunkArg ch,
         if (live[u]) acc[((c + u - G.col0) * kMaxChunks + ln.t) * 32 + ln.j] = s[u];
 }
 
-// Split mode (rows with many entries, where recomputing a neighbour's p costs
-// two gathers): iteration t as three streaming/gathering kernels
-//   k_cg_p : x += fl(alpha_{t-1} p_{t-1}) (pending columns); p_t = fl(fl(beta p) + r)
-//   k_cg_q : q_t = L_reg p_t (gathers of the stored p), q stored; chains of dot(p, q)
-//   k_cg_upd<STOREQ>: r -= fl(alpha q) streaming q
-template <bool FIRST, int CPL>
-__global__ void __launch_bounds__(256) k_cg_p(CgGeom G, ChunkArg ch, const double *__restrict__ R,
-                                              const double *__restrict__ Pold,
-                                              double *__restrict__ Pnew, double *__restrict__ X,
-                                              const double *__restrict__ rho,
-                                              const double *__restrict__ rho_prev,
-                                              const double *__restrict__ alpha,
-                                              const int32_t *__restrict__ active,
-                                              const int32_t *__restrict__ xstep, int32_t it) {
-    const CgLane ln = cg_lane<CPL>(G);
-    if (!ln.ok) return;
-    const int64_t ld = G.ld, c = ln.c;
-    bool live[CPL], xp[CPL];
-    double beta[CPL], al[CPL];
-    bool any_live = false, any_x = false;
-#pragma unroll
-    for (int u = 0; u < CPL; ++u) {
-        const bool in = (c + u) < G.col1;
-        live[u] = in && active[c + u];
-        xp[u] = !FIRST && in && xstep[c + u] == it - 1;
-        beta[u] = (!FIRST && live[u]) ? rho[c + u] / rho_prev[c + u] : 0.0;
-        al[u] = xp[u] ? alpha[c + u] : 0.0;
-        any_live = any_live || live[u];
-        any_x = any_x || xp[u];
-    }
-    if (!any_live && !any_x) return;
-    const int64_t a = ch.a[ln.t], L = ch.len[ln.t];
-    for (int64_t row = a + ln.j; row < a + L; row += 32) {
-        const int64_t o = row * ld + c;
-        Vec<CPL> po, rv;
-        if (!FIRST) po.load(Pold + o);
-        if (!FIRST && any_x) {
-            Vec<CPL> xv;
-            xv.load(X + o);
-#pragma unroll
-            for (int u = 0; u < CPL; ++u)
-                if (xp[u]) {
-                    double t1 = al[u] * po.v[u];
-                    xv.v[u] = xv.v[u] + t1;
-                }
-            xv.store(X + o);
-        }
-        if (!any_live) continue;
-        rv.load(R + o);
-        Vec<CPL> pw;
-#pragma unroll
-        for (int u = 0; u < CPL; ++u) {
-            double pn;
-            if (FIRST) {
-                pn = rv.v[u];
-            } else {
-                double pb = po.v[u] * beta[u];
-                pn = pb + rv.v[u];
-            }
-            pw.v[u] = pn;
-        }
-        if (CPL == 1 || (live[0] && live[CPL - 1])) {
-            pw.store(Pnew + o);
-        } else {
-#pragma unroll
-            for (int u = 0; u < CPL; ++u)
-                if (live[u]) Pnew[o + u] = pw.v[u];
-        }
-    }
-}
-
-// k_cg_p without a reduction, so it streams flat: threads own a column pair
+// Split modes (rows with many entries, where recomputing a neighbour's p costs
+// two gathers, or few columns, where the chains give too few waves):
+//   k_cg_p_flat : x += fl(alpha_{t-1} p_{t-1}) (pending columns); p_t = fl(fl(beta p) + r)
+//   k_cg_q (mode 2) : q_t = L_reg p_t (gathers of the stored p), q stored, dot(p, q) chains
+//   k_spmv + k_dot_acc (mode 3) : the same, SpMV in column-block-major order
+//   k_cg_upd<STOREQ> : r -= fl(alpha q) streaming q
+// The p update has no reduction, so it streams flat: threads own a column pair
 // (16 B, flags loaded once), blockIdx.y a band of kFlatRows rows, rows
 // walked in order -- each wave reads 1 KB contiguous per row.
 static constexpr int kFlatRows = 16;
@@ -1400,11 +1335,8 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
     } while (0)
 #define GS_PQ_S(F, C) \
     if (storeq) GS_PQ(F, C, true); else GS_PQ(F, C, false)
-#define GS_P(F, C)                                                                          \
-    k_cg_p<F, C><<<grid, block, 0, c->stream>>>(G, ch, Rr, Pold, Pnew, X, cp.rho, cp.rho_prev, \
-                                               cp.alpha, cp.active, cp.xstep, it)
 #define GS_Q(C) k_cg_q<C><<<grid, block, 0, c->stream>>>(G, ch, lp, li, lv, Pnew, Qfull, cp.active, acc)
-            if (mode == 3) {
+            if (mode >= 2) {
                 const dim3 pg((unsigned)(((ncols + 1) / 2 + 255) / 256),
                               (unsigned)((n + kFlatRows - 1) / kFlatRows));
                 if (it == 0)
@@ -1415,12 +1347,6 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
                     k_cg_p_flat<false><<<pg, 256, 0, c->stream>>>(G, Rr, Pold, Pnew, X, cp.rho,
                                                                   cp.rho_prev, cp.alpha, cp.active,
                                                                   cp.xstep, it);
-            } else if (mode == 2) {
-                if (it == 0) {
-                    if (cpl == 2) GS_P(true, 2); else GS_P(true, 1);
-                } else {
-                    if (cpl == 2) GS_P(false, 2); else GS_P(false, 1);
-                }
             }
             if (mode >= 2) {
                 prof_end(c, t0, "cg_p", (it == 0 ? 16.0 : 40.0) * n * ncols);
@@ -1451,7 +1377,6 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             } else {
                 if (cpl == 2) { GS_PQ_S(false, 2); } else { GS_PQ_S(false, 1); }
             }
-#undef GS_P
 #undef GS_Q
 #undef GS_PQ_S
 #undef GS_PQ
