@@ -110,6 +110,66 @@ __global__ void k_fill_u8(uint8_t *p, int64_t n, uint8_t v) {
         p[i] = v;
 }
 
+// Per-node argmax of the incident columns (sparsify_degree_aware phase 1,
+// core.py:415-428 with min_edges_per_node = 1): pick[u] = the column of the
+// unique maximum, -1 if u has no column, -2 when np.argsort's order decides
+// (several columns at the maximum, or a NaN score) -- the caller resolves
+// those nodes with the reference's own call.
+__global__ void k_seg_init(int64_t n, unsigned long long *__restrict__ mkey,
+                           unsigned long long *__restrict__ cnt, unsigned long long *__restrict__ ncol,
+                           int *__restrict__ nan, int64_t *__restrict__ idx) {
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        mkey[u] = 0ull;
+        cnt[u] = 0ull;
+        ncol[u] = 0ull;
+        nan[u] = 0;
+        idx[u] = -1;
+    }
+}
+
+__global__ void k_seg_max(const double *__restrict__ s, const int64_t *__restrict__ src, int64_t E,
+                          unsigned long long *__restrict__ mkey, unsigned long long *__restrict__ ncol,
+                          int *__restrict__ nan) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t u = src[i];
+        const double x = s[i];
+        atomicAdd(&ncol[u], 1ull);
+        if (x != x) atomicOr(&nan[u], 1);
+        else atomicMax(&mkey[u], (unsigned long long)order_key(x));
+    }
+}
+
+__global__ void k_seg_count(const double *__restrict__ s, const int64_t *__restrict__ src,
+                            int64_t E, const unsigned long long *__restrict__ mkey,
+                            unsigned long long *__restrict__ cnt, int64_t *__restrict__ idx) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t u = src[i];
+        const double x = s[i];
+        if (x == x && order_key(x) == mkey[u]) {
+            atomicAdd(&cnt[u], 1ull);
+            idx[u] = i;  // the only writer when the maximum is unique
+        }
+    }
+}
+
+__global__ void k_seg_pick(int64_t n, const unsigned long long *__restrict__ cnt,
+                           const unsigned long long *__restrict__ ncol, const int *__restrict__ nan,
+                           const int64_t *__restrict__ idx, int64_t *__restrict__ pick) {
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
+         u += (int64_t)gridDim.x * blockDim.x)
+        pick[u] = ncol[u] == 0 ? -1 : (nan[u] || cnt[u] != 1) ? -2 : idx[u];
+}
+
+__global__ void k_seg_check(const int64_t *__restrict__ src, int64_t E, int64_t n,
+                            int *__restrict__ bad) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x)
+        if (src[i] < 0 || src[i] >= n) atomicOr(bad, 1);
+}
+
 }  // namespace gs
 
 using namespace gs;
@@ -169,5 +229,47 @@ extern "C" int gs_topk_mask(gs_ctx *c, const double *scores, int s_loc, int64_t 
         if (cut) *cut = hcut;
         if (n_beyond) *n_beyond = hbeyond;
         if (n_tied) *n_tied = htied;
+    });
+}
+
+extern "C" int gs_segment_argmax(gs_ctx *c, const double *scores, int s_loc, int64_t nscores,
+                                 const int64_t *src, int src_loc, int64_t E, int64_t n,
+                                 int64_t *pick, int pick_loc) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        GS_CHECK(n >= 0 && E >= 0, GS_EINVAL, "negative n/E");
+        GS_CHECK(E <= nscores, GS_EINVAL,
+                 "index %lld is out of bounds for axis 0 with size %lld (scores are per CSR "
+                 "entry, columns per edge_index)", (long long)(E ? E - 1 : 0), (long long)nscores);
+        GS_HIP(hipSetDevice(c->device));
+        hipStream_t st = c->stream;
+        const double *ds = (const double *)to_device(c, c->buf("seg_s"), scores,
+                                                     sizeof(double) * (E ? E : 1), s_loc);
+        const int64_t *dsrc = (const int64_t *)to_device(c, c->buf("seg_src"), src,
+                                                         sizeof(int64_t) * (E ? E : 1), src_loc);
+        int64_t *dpick = (int64_t *)out_device(c, c->buf("seg_pick"), pick,
+                                               sizeof(int64_t) * (n ? n : 1), pick_loc);
+        auto *mkey = (unsigned long long *)c->buf("seg_mkey").ensure(8 * (n ? n : 1));
+        auto *cnt = (unsigned long long *)c->buf("seg_cnt").ensure(8 * (n ? n : 1));
+        auto *ncol = (unsigned long long *)c->buf("seg_ncol").ensure(8 * (n ? n : 1));
+        auto *nan = (int *)c->buf("seg_nan").ensure(4 * (n ? n : 1) + 64);
+        int *bad = nan + (n ? n : 1);
+        auto *idx = (int64_t *)c->buf("seg_idx").ensure(8 * (n ? n : 1));
+        GS_HIP(hipMemsetAsync(bad, 0, 4, st));
+        if (E) k_seg_check<<<grid_for(E, 256, 8192), 256, 0, st>>>(dsrc, E, n, bad);
+        int hbad = 0;
+        GS_HIP(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, st));
+        GS_HIP(hipStreamSynchronize(st));
+        GS_CHECK(!hbad, GS_EINVAL, "edge_index source out of range [0, %lld)", (long long)n);
+        hipEvent_t t0 = prof_begin(c);
+        if (n) k_seg_init<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, mkey, cnt, ncol, nan, idx);
+        if (E) {
+            k_seg_max<<<grid_for(E, 256, 8192), 256, 0, st>>>(ds, dsrc, E, mkey, ncol, nan);
+            k_seg_count<<<grid_for(E, 256, 8192), 256, 0, st>>>(ds, dsrc, E, mkey, cnt, idx);
+        }
+        if (n) k_seg_pick<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, cnt, ncol, nan, idx, dpick);
+        GS_HIP(hipGetLastError());
+        prof_end(c, t0, "segment_argmax", 8.0 * 3 * (double)E + 8.0 * (double)n);
+        finish_out(c, pick, dpick, sizeof(int64_t) * n, pick_loc);
     });
 }

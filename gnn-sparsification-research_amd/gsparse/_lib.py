@@ -58,6 +58,7 @@ SIGNATURES = {
     "gs_er_split": (_int, [_i64, _i32, _vp]),
     "gs_topk_mask": (_int, [_vp, _vp, _int, _i64, _i64, _i64, _int, _vp, _int,
                             ctypes.POINTER(_f64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
+    "gs_segment_argmax": (_int, [_vp, _vp, _int, _i64, _vp, _int, _i64, _i64, _vp, _int]),
     "gs_metric_backbone": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _int, _f64, _vp, _int,
                                   ctypes.POINTER(_i64)]),
     "gs_metric_backbone_part": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _int, _f64, _int, _int,

@@ -29,7 +29,7 @@ from ._lib import Context
 from .data import Data
 from .engine import Engine
 from .metric_backbone import compute_metric_backbone
-from .selection import degree_aware_mask, numpy_topk_mask, sampled_mask
+from .selection import degree_aware_mask_device, numpy_topk_mask, sampled_mask
 
 
 def _device_index(device) -> int | None:
@@ -259,7 +259,8 @@ class GraphSparsifier:
         Same result as the reference's O(N*E) loops: each node's guaranteed
         columns are chosen by the same ``np.argsort`` over its incident scores,
         and the fill takes the first non-guaranteed entries of
-        ``np.argsort(scores)[::-1]`` (host, SURVEY §8(f) rank 1)."""
+        ``np.argsort(scores)[::-1]`` -- both on the device, with the reference's
+        own calls only where its argsort order decides."""
         if not 0 < retention_ratio <= 1:
             raise ValueError(f"retention_ratio must be in (0, 1], got {retention_ratio}")
         if retention_ratio == 1.0:
@@ -267,8 +268,9 @@ class GraphSparsifier:
                 return self.data.clone(), torch.ones(self.num_edges, dtype=torch.bool)
             return self.data.clone()
         scores = self.compute_scores(metric)
-        mask = degree_aware_mask(scores, self.data.edge_index.cpu().numpy(), self.num_nodes,
-                                 self.num_edges, retention_ratio, min_edges_per_node)
+        mask = degree_aware_mask_device(self._engine, scores, self.data.edge_index.cpu().numpy(),
+                                        self.num_nodes, self.num_edges, retention_ratio,
+                                        min_edges_per_node)
         sparse_edge_index = self.data.edge_index[:, torch.from_numpy(mask).to(
             self.data.edge_index.device)].to(self.device)
         sparse_data = self.data.clone()

@@ -220,6 +220,16 @@ class Engine:
         return self.er_scores(0, k, True)
 
     # -- selection ------------------------------------------------------------
+    def segment_argmax(self, scores: np.ndarray, src: np.ndarray, num_nodes: int) -> np.ndarray:
+        """gs_segment_argmax: per node the column of its unique top score, -1 (no
+        column) or -2 (np.argsort's order decides)."""
+        scores = np.ascontiguousarray(scores, dtype=np.float64)
+        src = np.ascontiguousarray(src, dtype=np.int64)
+        pick = np.empty(max(num_nodes, 1), dtype=np.int64)
+        self.ctx.call("gs_segment_argmax", ptr(scores), GS_HOST, int(scores.shape[0]), ptr(src),
+                      GS_HOST, int(src.shape[0]), int(num_nodes), ptr(pick), GS_HOST)
+        return pick[:num_nodes]
+
     def topk_mask(self, scores, num_edges: int, num_keep: int, keep_lowest: bool):
         """Device mask + (cut, #beyond, #tied) -- see gs_topk_mask."""
         scores = np.ascontiguousarray(scores, dtype=np.float64) if isinstance(scores, np.ndarray) \

@@ -71,6 +71,49 @@ def degree_aware_mask(scores: np.ndarray, edge_index: np.ndarray, num_nodes: int
     return mask
 
 
+def degree_aware_mask_device(engine, scores: np.ndarray, edge_index: np.ndarray,
+                             num_nodes: int, num_edges: int, retention_ratio: float,
+                             min_edges_per_node: int = 1) -> np.ndarray:
+    """degree_aware_mask with both phases on the MI355X; the same result.
+
+    Phase 1: gs_segment_argmax gives every node's unique top column; nodes
+    where np.argsort's order decides (ties at the maximum, NaN) take the
+    reference's own call.  Phase 2: a device radix select over the scores with
+    the guaranteed columns removed; an ambiguous tie block at the cut (or any
+    NaN) takes the reference's own descending argsort walk."""
+    scores = np.asarray(scores, dtype=np.float64)
+    src = np.ascontiguousarray(np.asarray(edge_index)[0], dtype=np.int64)
+    if min_edges_per_node != 1 or num_edges > len(scores) or np.isnan(scores).any():
+        return degree_aware_mask(scores, edge_index, num_nodes, num_edges, retention_ratio,
+                                 min_edges_per_node)
+    num_keep = int(num_edges * retention_ratio)
+    pick = engine.segment_argmax(scores, src[:num_edges], num_nodes)
+    mask = np.zeros(num_edges, dtype=bool)
+    mask[pick[pick >= 0]] = True
+    amb = np.nonzero(pick == -2)[0]
+    if len(amb):
+        order = np.argsort(src, kind="stable")
+        bounds = np.searchsorted(src[order], np.arange(num_nodes + 1))
+        for node in amb:
+            incident = order[bounds[node]:bounds[node + 1]]
+            mask[incident[np.argsort(scores[incident])[-1:]]] = True
+    have = int(mask.sum())
+    if have >= num_keep:
+        return mask
+    k2 = num_keep - have
+    masked = scores.copy()
+    masked[np.nonzero(mask)[0]] = -np.inf
+    sel, cut, beyond, tied = engine.topk_mask(masked, num_edges, k2, False)
+    need = k2 - beyond
+    if (0 < need < tied) or cut == -np.inf:
+        # the reference's own walk: first non-guaranteed of argsort(scores)[::-1]
+        sorted_indices = np.argsort(scores)[::-1]
+        cand = sorted_indices[~mask[sorted_indices]]
+        mask[cand[:k2]] = True
+        return mask
+    return mask | sel
+
+
 def numpy_topk_mask(scores: np.ndarray, num_edges: int, num_keep: int,
                     keep_lowest: bool) -> np.ndarray:
     """core.py:233-240 verbatim: the reference's unstable argsort tie order."""

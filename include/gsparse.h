@@ -143,6 +143,16 @@ int gs_topk_mask(gs_ctx *ctx, const double *scores, int s_loc, int64_t nnz, int6
  * distance d from src in the undirected graph of the src<dst columns
  * (min weight over duplicates), keep iff d == inf or w[idx] <= d + eps.
  * n_relax (optional) returns the number of edge relaxations performed. */
+/* sparsify_degree_aware phase 1 (core.py:415-428, min_edges_per_node = 1):
+ * for every node u, pick[u] = the edge_index column i (src[i] == u) holding
+ * the unique maximum of scores[i], -1 if u has no column, -2 when the
+ * reference's np.argsort order decides (ties at the maximum or a NaN).
+ * scores are indexed by column as the reference indexes them (needs E <=
+ * nscores, else GS_EINVAL, the reference's IndexError). */
+int gs_segment_argmax(gs_ctx *ctx, const double *scores, int s_loc, int64_t nscores,
+                      const int64_t *src, int src_loc, int64_t E, int64_t n, int64_t *pick,
+                      int pick_loc);
+
 int gs_metric_backbone(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src,
                        const int64_t *dst, const double *w, int loc, double eps,
                        uint8_t *keep, int keep_loc, int64_t *n_relax);

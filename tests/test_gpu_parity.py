@@ -288,6 +288,29 @@ def test_backbone_parts_sum_to_whole(gs, nparts):
     assert np.array_equal(tot.astype(bool), whole)
 
 
+@pytest.mark.parametrize("metric", ["jaccard", "degree", "approx_er"])
+def test_degree_aware_device_equals_reference_walk(gs, metric):
+    """Device phases (segment argmax + radix select) vs the reference's loops
+    restated on the host (selection.degree_aware_mask), ties included."""
+    from gsparse import graphs
+    from gsparse.selection import degree_aware_mask, degree_aware_mask_device
+
+    ei, n = graphs.rmat(12, 8, seed=6), 1 << 12
+    data = gs.Data(edge_index=torch.from_numpy(ei), num_nodes=n)
+    sp_ = gs.GraphSparsifier(data, "cpu")
+    if metric == "approx_er":
+        sc = sp_._engine.approx_er(epsilon=0.9, blas_threads=1)
+    else:
+        sc = sp_.compute_scores(metric)
+    E = ei.shape[1]
+    pick = sp_._engine.segment_argmax(sc, ei[0], n)
+    assert (pick == -2).any() or metric == "approx_er"
+    for r in [0.05, 0.2, 0.5, 0.8]:
+        ref = degree_aware_mask(sc, ei, n, E, r)
+        dev = degree_aware_mask_device(sp_._engine, sc, ei, n, E, r)
+        assert np.array_equal(ref, dev), (metric, r)
+
+
 def test_featcos_1433_bow_vs_oracle(gs):
     from gsparse import graphs
 
