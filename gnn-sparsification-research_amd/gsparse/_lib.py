@@ -63,6 +63,7 @@ SIGNATURES = {
                                   ctypes.POINTER(_i64)]),
     "gs_metric_backbone_part": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _int, _f64, _int, _int,
                                        _vp, _int, ctypes.POINTER(_i64)]),
+    "gs_exact_er": (_int, [_vp, _vp, _int, ctypes.POINTER(_i32)]),
 }
 
 

@@ -165,9 +165,7 @@ class GraphSparsifier:
         elif metric_key == "adamic_adar":
             scores = eng.adamic_adar()
         elif metric_key == "effective_resistance":
-            from .metrics import calculate_effective_resistance_scores
-
-            scores = calculate_effective_resistance_scores(self.adj)
+            scores = eng.exact_er()
         elif metric_key == "approx_effective_resistance":
             scores = eng.approx_er()
         elif metric_key == "random":

@@ -220,6 +220,15 @@ class Engine:
         return self.er_scores(0, k, True)
 
     # -- selection ------------------------------------------------------------
+    def exact_er(self, out=None):
+        """calculate_effective_resistance_scores (metrics.py:124-175) -- gs_exact_er:
+        dense fp64-MFMA Newton-Schulz inverse of L + sum_C J_C/|C|."""
+        o, loc = self._out(0, self.nnz, out)
+        it = ctypes.c_int32(0)
+        self.ctx.call("gs_exact_er", ptr(o), loc, ctypes.byref(it))
+        self.exact_er_iterations = it.value
+        return o
+
     def segment_argmax(self, scores: np.ndarray, src: np.ndarray, num_nodes: int) -> np.ndarray:
         """gs_segment_argmax: per node the column of its unique top score, -1 (no
         column) or -2 (np.argsort's order decides)."""

@@ -91,20 +91,16 @@ def calculate_adamic_adar_scores(adj: sp.csr_matrix) -> NDArray[np.float64]:
 
 
 def calculate_effective_resistance_scores(adj: sp.csr_matrix) -> NDArray[np.float64]:
-    """EXACT effective resistance via the dense pseudoinverse (metrics.py:124-175).
+    """EXACT effective resistance (metrics.py:124-175), dense, on the MI355X.
 
-    Outside the accelerated path (dense O(n^3)): evaluated
-    with the reference's own NumPy/LAPACK formula, small graphs only."""
-    a = sp.csr_matrix(adj)
-    n = a.shape[0]
-    degrees = np.array(a.sum(axis=1)).flatten()
-    L = sp.diags(degrees, format="csr") - a
-    L_reg = L + 1e-10 * sp.eye(n, format="csr")
-    L_pinv = np.linalg.pinv(L_reg.toarray())
-    rows, cols = a.nonzero()
-    r_eff = L_pinv[rows, rows] + L_pinv[cols, cols] - 2.0 * L_pinv[rows, cols]
-    r_eff = np.maximum(r_eff, 1e-10)
-    return r_eff.astype(np.float64)
+    The reference reads R(u,v) = P_uu + P_vv - 2 P_uv off pinv(L + 1e-10 I); this
+    reads it off inv(L + sum_C J_C/|C|) (equal in exact arithmetic for every
+    edge, whose endpoints share a component), inverted by Newton-Schulz on fp64
+    MFMA (gs_exact_er).  Agrees with the reference to its own pinv rounding
+    noise (<= 1e-4 relative on the fixtures; DESIGN.md §Exact ER).  Symmetric
+    adjacency with n <= 32768 only (NotImplementedError otherwise)."""
+    eng, perm = _engine(adj)
+    return _unpermute(eng.exact_er(), perm)
 
 
 def calculate_approx_effective_resistance_scores(

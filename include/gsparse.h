@@ -164,6 +164,15 @@ int gs_metric_backbone_part(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *sr
                             const int64_t *dst, const double *w, int loc, double eps, int part,
                             int nparts, uint8_t *keep, int keep_loc, int64_t *n_relax);
 
+/* Exact effective resistance of the resident (symmetric) graph, one score per
+ * CSR entry.  Replaces calculate_effective_resistance_scores (metrics.py:124-175:
+ * dense pinv of L + 1e-10 I).  Computed as (M^-1)_uu + (M^-1)_vv - 2 (M^-1)_uv with
+ * M = L + sum_C J_C/|C| (one lift per connected component), M^-1 by fp64-MFMA
+ * Newton-Schulz; max(., 1e-10) as the reference clamps.  Dense: n <= 32768
+ * (GS_EUNSUPPORTED above, and for a directed adjacency).  *iterations (may be
+ * NULL) receives the Newton-Schulz step count. */
+int gs_exact_er(gs_ctx *ctx, double *out, int out_loc, int32_t *iterations);
+
 #ifdef __cplusplus
 }
 #endif

@@ -238,6 +238,33 @@ def er_from_z(indptr, indices, Z):
     return out
 
 
+def exact_er(indptr, indices, data, n, lifted=True):
+    """calculate_effective_resistance_scores (metrics.py:124-175).
+
+    lifted=False restates the reference literally: pinv(L + 1e-10 I) by SVD
+    (metrics.py:159-169), R = P_uu + P_vv - 2 P_uv, clamp 1e-10 (:171-173).
+    lifted=True is the well-conditioned form the device computes: inv(M) with
+    M = L + sum_C J_C/|C| -- identical in exact arithmetic for u, v in one
+    component, without the 1e10/|C| direction whose rounding is the
+    reference's own 1e-6..5e-5 noise (DESIGN.md §Exact ER)."""
+    from scipy.sparse.csgraph import connected_components
+
+    a = sp.csr_matrix((np.asarray(data, dtype=np.float64), indices, indptr), shape=(n, n))
+    deg = np.asarray(a.sum(axis=1)).ravel()
+    L = (sp.diags(deg) - a).toarray()
+    if lifted:
+        _, lab = connected_components(a, directed=False)
+        size = np.bincount(lab)
+        L += (lab[:, None] == lab[None, :]) / size[lab][:, None]
+        P = np.linalg.inv(L)
+    else:
+        P = np.linalg.pinv(L + 1e-10 * np.eye(n))
+    rows = np.repeat(np.arange(n), np.diff(indptr))
+    cols = np.asarray(indices, dtype=np.int64)
+    r = P[rows, rows] + P[cols, cols] - 2.0 * P[rows, cols]
+    return np.maximum(r, 1e-10)
+
+
 # ----------------------------------------------------------------------------
 # selection (core.py)
 def topk_mask(scores, num_edges, retention_ratio, keep_lowest=False, kind=None):

@@ -14,7 +14,8 @@ import pytest
 import torch
 
 import gsparse_oracle as O
-from conftest import bits_equal, golden_features, golden_names, load_golden
+from conftest import (EXACT_ER_ATOL, bits_equal, exact_er_golden, exact_er_names, golden_features,
+                      golden_names, load_golden)
 
 pytestmark = pytest.mark.gpu
 
@@ -414,3 +415,75 @@ def test_approx_er_device_rng_roman_full(gs):
     sp_, _ = make(gs, g, with_x=False)
     er = sp_._engine.approx_er(blas_threads=1, rng_mode="device")
     assert bits_equal(er, g["scores_approx_er"])
+
+
+# ---- exact effective resistance (metrics.py:124-175) on fp64 MFMA ----------
+@pytest.mark.parametrize("name", exact_er_names())
+def test_exact_er_device(gs, name):
+    """gs_exact_er vs the reference golden (within the reference's own pinv noise,
+    EXACT_ER_ATOL) and vs the lifted oracle (rtol 1e-9: the device's only error is
+    Newton-Schulz rounding, ~cond(M) * eps)."""
+    import scipy.sparse as sp
+
+    g = load_golden(name)
+    n = int(g["num_nodes"])
+    adj = sp.csr_matrix((g["data"], g["indices"], g["indptr"]), shape=(n, n))
+    er = gs.calculate_effective_resistance_scores(adj)
+    ref = exact_er_golden(name)
+    assert er.dtype == np.float64 and er.shape == ref.shape
+    assert np.max(np.abs(er - ref), initial=0.0) <= EXACT_ER_ATOL
+    lifted = O.exact_er(g["indptr"], g["indices"], g["data"], n, lifted=True)
+    np.testing.assert_allclose(er, lifted, rtol=1e-9, atol=1e-12)
+
+
+def test_exact_er_through_sparsifier(gs):
+    g = load_golden("karate_test")
+    sp_, _ = make(gs, g, with_x=False)
+    er = sp_.compute_scores("effective_resistance")
+    assert np.max(np.abs(er - g["scores_effective_resistance"])) <= EXACT_ER_ATOL
+    _, m = sp_.sparsify("effective_resistance", 0.5, return_mask=True)
+    assert m.dtype == torch.bool and int(m.sum()) > 0
+
+
+@pytest.mark.parametrize("n,blocks", [(3000, 5), (4100, 1), (70, 3)])
+def test_exact_er_components_and_padding(gs, n, blocks):
+    """Several components (plus isolated nodes), weights, n not a multiple of 64."""
+    import scipy.sparse as sp
+
+    rng = np.random.default_rng(n)
+    parts = np.array_split(np.arange(n - 3), blocks)
+    rows, cols = [], []
+    for p in parts:
+        m = len(p)
+        a = rng.integers(0, m, 4 * m)
+        b = rng.integers(0, m, 4 * m)
+        keep = a != b
+        rows.append(p[a[keep]]), cols.append(p[b[keep]])
+        rows.append(p[:-1]), cols.append(p[1:])  # a path keeps each part connected
+    r = np.concatenate(rows)
+    c = np.concatenate(cols)
+    w = rng.uniform(0.5, 2.0, len(r))
+    A = sp.coo_matrix((w, (r, c)), shape=(n, n)).tocsr()
+    A = (A + A.T).tocsr()
+    A.sum_duplicates()
+    er = gs.calculate_effective_resistance_scores(A)
+    lifted = O.exact_er(A.indptr, A.indices, A.data, n, lifted=True)
+    np.testing.assert_allclose(er, lifted, rtol=1e-9, atol=1e-12)
+
+
+def test_exact_er_rejects_directed(gs):
+    import scipy.sparse as sp
+
+    A = sp.csr_matrix(np.array([[0, 1, 0], [0, 0, 1], [1, 0, 0]], dtype=np.float64))
+    with pytest.raises(NotImplementedError):
+        gs.calculate_effective_resistance_scores(A)
+    B = sp.csr_matrix(np.array([[0, 1.0], [2.0, 0]]))
+    with pytest.raises(NotImplementedError):
+        gs.calculate_effective_resistance_scores(B)
+
+
+def test_exact_er_empty_graph(gs):
+    import scipy.sparse as sp
+
+    er = gs.calculate_effective_resistance_scores(sp.csr_matrix((5, 5)))
+    assert er.shape == (0,)
