@@ -2,17 +2,22 @@
 // metrics.py:124-175) on the device, fp64 MFMA.
 //
 // The reference takes the dense pseudo-inverse of L + 1e-10 I by SVD and reads
-// R(u,v) = P_uu + P_vv - 2 P_uv.  For u, v in one connected component C every
-// component-constant term cancels in that form, so it equals the same form on
-// M^{-1} with M = L + sum_C J_C / |C| (J_C = 1_C 1_C^T): M is SPD with the
-// null vectors of L lifted to eigenvalue 1, and its condition number is that
-// of L on the complement (no 1e10 direction).  The reference's own value
-// carries the rounding of its 1e10/|C| component (1e-6 .. 5e-5 absolute on the
-// fixtures); this computation is within ~1e-12 of an exact one.
+// R(u,v) = P_uu + P_vv - 2 P_uv.  Within a connected component that is the
+// effective resistance, which grounding one node g per component computes
+// exactly: with M = L with row/column g replaced by the identity (SPD, sparse)
+// and G = M^{-1} with row/column g zeroed, R(u,v) = G_uu + G_vv - 2 G_uv.  The
+// reference's own value carries the rounding of its 1e10/|C| direction (1e-6 ..
+// 5e-5 absolute on the fixtures); this computation has none of it.  g = the
+// component's node of largest degree (smallest id on ties).
 //
-// M^{-1} by Newton-Schulz, X <- 2X - X (M X), X0 = I / ||M||_inf (Gershgorin, so
-// every eigenvalue of X0 M is in (0, 1]): two n^3 fp64 GEMMs per step on
-// v_mfma_f64_16x16x4_f64, residual max|I - M X| checked every step.
+// M^{-1} by Newton-Schulz in its symmetric form, X <- 2X - X (M X) with
+// X0 = I / ||M||_inf (Gershgorin, so every eigenvalue of X0 M is in (0, 1]):
+// S = M X is a sparse-times-dense product (nnz N per step, HBM-bound), X S =
+// X M X is exactly symmetric in exact arithmetic for any symmetric X, so only
+// its upper-triangle tiles run (N^3 flops per step on v_mfma_f64_16x16x4_f64)
+// and X stays exactly symmetric.  ||I - M X||_F is folded into the S kernel.
+#include <cmath>
+
 #include "gs_internal.hpp"
 
 namespace gs {
@@ -20,7 +25,33 @@ namespace gs {
 static constexpr int kGemmTile = 64;  // 64x64 output tile per 256-thread workgroup
 static constexpr int kGemmK = 16;     // K slice staged in LDS
 
-// C = alpha * A * B + beta * Cin  (N x N row-major, N a multiple of 64, fp64)
+// Workgroup -> output tile.  Dispatch deals consecutive workgroup ids round-robin
+// over the 8 XCDs; regroup so each XCD walks a contiguous run of tiles (shared
+// A rows / B columns stay in its own L2).  SYM: only tiles bi <= bj (row-major
+// over the upper triangle), the result mirrored into (bj, bi).
+template <bool SYM>
+__device__ __forceinline__ void gemm_tile(int nb, int &bi, int &bj) {
+    const int nblk = gridDim.x;
+    int t = blockIdx.x;
+    if ((nblk & 7) == 0) t = (t & 7) * (nblk >> 3) + (t >> 3);
+    if (!SYM) {
+        bi = t / nb;
+        bj = t % nb;
+        return;
+    }
+    // row bi starts at s(bi) = bi*nb - bi*(bi-1)/2
+    const double q = 2.0 * nb + 1.0;
+    int r = (int)((q - sqrt(q * q - 8.0 * t)) * 0.5);
+    while (r > 0 && (int64_t)r * nb - (int64_t)r * (r - 1) / 2 > t) --r;
+    while ((int64_t)(r + 1) * nb - (int64_t)(r + 1) * r / 2 <= t) ++r;
+    bi = r;
+    bj = r + (t - (r * nb - r * (r - 1) / 2));
+}
+
+// C = alpha * A * B + beta * Cin  (N x N row-major, N a multiple of 64, fp64).
+// SYM: the product is known symmetric (A, B, Cin polynomials in one symmetric
+// matrix): half the tiles, each written to both triangles.
+template <bool SYM>
 __global__ void __launch_bounds__(256) k_dgemm(int64_t N, const double *__restrict__ A,
                                                const double *__restrict__ B, double alpha,
                                                double beta, const double *__restrict__ Cin,
@@ -28,7 +59,9 @@ __global__ void __launch_bounds__(256) k_dgemm(int64_t N, const double *__restri
     __shared__ double As[kGemmTile][kGemmK + 1];
     __shared__ double Bs[kGemmK][kGemmTile + 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t r0 = (int64_t)blockIdx.y * kGemmTile, c0 = (int64_t)blockIdx.x * kGemmTile;
+    int bi, bj;
+    gemm_tile<SYM>((int)(N / kGemmTile), bi, bj);
+    const int64_t r0 = (int64_t)bi * kGemmTile, c0 = (int64_t)bj * kGemmTile;
     const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;  // the wave's 32x32 quadrant
     typedef double d4 __attribute__((ext_vector_type(4)));
     d4 acc[2][2];
@@ -74,7 +107,9 @@ __global__ void __launch_bounds__(256) k_dgemm(int64_t N, const double *__restri
                 const int64_t col = c0 + wc + j * 16 + (lane & 15);
                 const int64_t o = row * N + col;
                 const double v = alpha * acc[i][j][r];
-                C[o] = beta != 0.0 ? v + beta * Cin[o] : v;
+                const double w = beta != 0.0 ? v + beta * Cin[o] : v;
+                C[o] = w;
+                if (SYM && bi != bj) C[col * N + row] = w;
             }
 }
 
@@ -117,55 +152,55 @@ __global__ void k_cc_jump(int64_t n, int32_t *__restrict__ lab) {
     }
 }
 
-__global__ void k_cc_size(int64_t n, const int32_t *__restrict__ lab, int32_t *__restrict__ size) {
-    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
-         u += (int64_t)gridDim.x * blockDim.x)
-        atomicAdd(&size[lab[u]], 1);
-}
-
-// M = J-lift (1/|C| within a component), identity on the padding
-__global__ void k_er_mfill(int64_t n, int64_t N, const int32_t *__restrict__ lab,
-                           const int32_t *__restrict__ size, double *__restrict__ M) {
-    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < N * N;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = idx / N, j = idx % N;
-        double v = 0.0;
-        if (i < n && j < n) {
-            if (lab[i] == lab[j]) v = 1.0 / (double)size[lab[i]];
-        } else if (i == j) {
-            v = 1.0;
-        }
-        M[idx] = v;
-    }
-}
-
-// + L = D - A (degree = row sum of the multiplicities, metrics.py:159-163)
-__global__ void k_er_laplace(int64_t n, int64_t N, const int64_t *__restrict__ ip,
-                             const int32_t *__restrict__ ix, const double *__restrict__ d,
-                             double *__restrict__ M) {
+// grounded node per component: largest row length, smallest id on ties
+__global__ void k_er_ground_pick(int64_t n, const int64_t *__restrict__ ip,
+                                 const int32_t *__restrict__ lab,
+                                 unsigned long long *__restrict__ best) {
     for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
          u += (int64_t)gridDim.x * blockDim.x) {
-        double deg = 0.0;
-        for (int64_t e = ip[u]; e < ip[u + 1]; ++e) deg += d[e];
-        for (int64_t e = ip[u]; e < ip[u + 1]; ++e) M[u * N + ix[e]] -= d[e];
-        M[u * N + u] += deg;
+        const unsigned long long key = ((unsigned long long)(ip[u + 1] - ip[u]) << 32) |
+                                       (unsigned long long)(0xffffffffu - (uint32_t)u);
+        atomicMax(&best[lab[u]], key);
     }
 }
 
-// Gershgorin bound max_i sum_j |M_ij| (one workgroup per row, max via bits)
-__global__ void k_er_rownorm(int64_t N, const double *__restrict__ M,
-                             unsigned long long *__restrict__ mx) {
-    __shared__ double part[256];
-    const int64_t i = blockIdx.x;
-    double s = 0.0;
-    for (int64_t j = threadIdx.x; j < N; j += blockDim.x) s += fabs(M[i * N + j]);
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
-        __syncthreads();
+// flag[u] = 1 for identity rows of M (grounded nodes and the padding up to N)
+__global__ void k_er_ground_mark(int64_t n, int64_t N, const int32_t *__restrict__ lab,
+                                 const unsigned long long *__restrict__ best,
+                                 uint8_t *__restrict__ flag) {
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < N;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        if (u >= n) {
+            flag[u] = 1;
+            continue;
+        }
+        const uint32_t g = 0xffffffffu - (uint32_t)(best[lab[u]] & 0xffffffffu);
+        flag[u] = g == (uint32_t)u;
     }
-    if (threadIdx.x == 0) atomicMax(mx, (unsigned long long)__double_as_longlong(part[0]));
+}
+
+// Gershgorin bound ||M||_inf (max via the bits of a non-negative double)
+__global__ void k_er_rownorm(int64_t n, const int64_t *__restrict__ ip,
+                             const int32_t *__restrict__ ix, const double *__restrict__ d,
+                             const uint8_t *__restrict__ flag, unsigned long long *__restrict__ mx) {
+    double m = 1.0;  // identity rows
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        if (flag[u]) continue;
+        double deg = 0.0, diag = 0.0, off = 0.0;
+        for (int64_t e = ip[u]; e < ip[u + 1]; ++e) {
+            deg += d[e];
+            if (ix[e] == u) diag += d[e];
+            else if (!flag[ix[e]]) off += d[e];
+        }
+        const double r = fabs(deg - diag) + off;
+        m = r > m ? r : m;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double t = __shfl_down(m, o, 64);
+        m = t > m ? t : m;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(mx, (unsigned long long)__double_as_longlong(m));
 }
 
 __global__ void k_er_xinit(int64_t N, const unsigned long long *__restrict__ mx,
@@ -176,32 +211,73 @@ __global__ void k_er_xinit(int64_t N, const unsigned long long *__restrict__ mx,
         X[idx] = (idx / N == idx % N) ? c : 0.0;
 }
 
-// max |I - T| (non-negative doubles order as their bits)
-__global__ void k_er_resid(int64_t N, const double *__restrict__ T,
-                           unsigned long long *__restrict__ mx) {
-    double m = 0.0;
-    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < N * N;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const double r = fabs((idx / N == idx % N ? 1.0 : 0.0) - T[idx]);
-        m = r > m ? r : m;
+// S = M X, row i of S from row i of the CSR: (deg_i - A_ii) X_i - sum A_ij X_j over
+// non-grounded j != i; S_i = X_i on identity rows.  One workgroup per (row,
+// 256-column slice); each block also leaves its share of ||I - S||_F^2.
+__global__ void __launch_bounds__(256) k_er_spmm(int64_t n, int64_t N, const int64_t *__restrict__ ip,
+                                                 const int32_t *__restrict__ ix,
+                                                 const double *__restrict__ d,
+                                                 const uint8_t *__restrict__ flag,
+                                                 const double *__restrict__ X,
+                                                 double *__restrict__ S, double *__restrict__ part) {
+    __shared__ double red[4];
+    const int64_t slices = (N + 255) / 256;
+    const int64_t i = blockIdx.x / slices;
+    const int64_t j = (blockIdx.x % slices) * 256 + threadIdx.x;
+    double v = 0.0;
+    if (j >= N) {
+        // past the last column: contributes nothing
+    } else if (flag[i]) {
+        v = X[i * N + j];
+    } else {
+        double deg = 0.0, diag = 0.0, acc = 0.0;
+        for (int64_t e = ip[i]; e < ip[i + 1]; ++e) {
+            const int32_t k = ix[e];
+            const double w = d[e];
+            deg += w;
+            if (k == i) diag += w;
+            else if (!flag[k]) acc += w * X[(int64_t)k * N + j];
+        }
+        v = (deg - diag) * X[i * N + j] - acc;
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        const double t = __shfl_down(m, o, 64);
-        m = t > m ? t : m;
-    }
-    if ((threadIdx.x & 63) == 0) atomicMax(mx, (unsigned long long)__double_as_longlong(m));
+    if (j < N) S[i * N + j] = v;
+    const double r = j < N ? (i == j ? 1.0 : 0.0) - v : 0.0;
+    double s2 = r * r;
+    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_down(s2, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s2;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-// r_eff in CSR order: (P_uu + P_vv) - 2 P_uv, then max(., 1e-10) (metrics.py:171-173)
+// ||I - S||_F from the per-block shares, folded in a fixed order (deterministic)
+__global__ void __launch_bounds__(256) k_er_resid_fin(const double *__restrict__ part, int64_t np,
+                                                      double *__restrict__ res) {
+    __shared__ double red[256];
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < np; i += 256) s += part[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *res = sqrt(red[0]);
+}
+
+// r_eff in CSR order: (G_uu + G_vv) - 2 G_uv, then max(., 1e-10) (metrics.py:171-173);
+// G = X with grounded rows/columns read as zero
 __global__ void k_er_exact_scores(int64_t N, const int32_t *__restrict__ rows,
                                   const int32_t *__restrict__ ix, int64_t nnz,
+                                  const uint8_t *__restrict__ flag,
                                   const double *__restrict__ X, double *__restrict__ out) {
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz;
          e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t u = rows[e], v = ix[e];
-        const double s = X[u * N + u] + X[v * N + v];
-        const double t = 2.0 * X[u * N + v];
-        const double r = s - t;
+        const bool fu = flag[u], fv = flag[v];
+        const double guu = fu ? 0.0 : X[u * N + u];
+        const double gvv = fv ? 0.0 : X[v * N + v];
+        const double guv = (fu || fv) ? 0.0 : X[u * N + v];
+        const double r = (guu + gvv) - 2.0 * guv;
         out[e] = r > 1e-10 ? r : 1e-10;
     }
 }
@@ -238,7 +314,6 @@ extern "C" int gs_exact_er(gs_ctx *c, double *out, int loc, int32_t *iterations)
                          "exact effective resistance needs symmetric edge weights");
             }
             auto *lab = (int32_t *)c->buf("xer_lab").ensure(4 * n);
-            auto *size = (int32_t *)c->buf("xer_size").ensure(4 * n);
             k_cc_init<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, lab);
             for (int round = 0; round < 4096; ++round) {
                 GS_HIP(hipMemsetAsync(flags, 0, 4, st));
@@ -251,49 +326,60 @@ extern "C" int gs_exact_er(gs_ctx *c, double *out, int loc, int32_t *iterations)
                 GS_HIP(hipStreamSynchronize(st));
                 if (!ch) break;
             }
-            GS_HIP(hipMemsetAsync(size, 0, 4 * n, st));
-            k_cc_size<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, lab, size);
+            const int64_t *ip = g.indptr.as<int64_t>();
+            const int32_t *ix = g.indices.as<int32_t>();
+            const double *dd = g.data.as<double>();
+            auto *best = (unsigned long long *)c->buf("xer_best").ensure(8 * n);
+            auto *flag = (uint8_t *)c->buf("xer_flag").ensure(N);
+            auto *mx = (unsigned long long *)c->buf("xer_mx").ensure(64);
+            GS_HIP(hipMemsetAsync(best, 0, 8 * n, st));
+            GS_HIP(hipMemsetAsync(mx, 0, 64, st));
+            k_er_ground_pick<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, ip, lab, best);
+            k_er_ground_mark<<<grid_for(N, 256, 8192), 256, 0, st>>>(n, N, lab, best, flag);
+            k_er_rownorm<<<grid_for(n, 256, 2048), 256, 0, st>>>(n, ip, ix, dd, flag, mx);
             const size_t mb = sizeof(double) * (size_t)N * (size_t)N;
-            double *M = (double *)c->buf("xer_M").ensure(mb);
             double *X = (double *)c->buf("xer_X").ensure(mb);
             double *X2 = (double *)c->buf("xer_X2").ensure(mb);
-            double *T = (double *)c->buf("xer_T").ensure(mb);
-            auto *mx = (unsigned long long *)c->buf("xer_mx").ensure(64);
-            k_er_mfill<<<grid_for(N * N, 256, 65536), 256, 0, st>>>(n, N, lab, size, M);
-            k_er_laplace<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, N, g.indptr.as<int64_t>(),
-                                                                g.indices.as<int32_t>(),
-                                                                g.data.as<double>(), M);
-            GS_HIP(hipMemsetAsync(mx, 0, 64, st));
-            k_er_rownorm<<<(unsigned)N, 256, 0, st>>>(N, M, mx);
+            double *S = (double *)c->buf("xer_S").ensure(mb);
+            const int64_t sblocks = N * ((N + 255) / 256);
+            auto *rpart = (double *)c->buf("xer_resid").ensure(8 * (sblocks + 1));
             k_er_xinit<<<grid_for(N * N, 256, 65536), 256, 0, st>>>(N, mx, X);
-            const dim3 gg((unsigned)(N / kGemmTile), (unsigned)(N / kGemmTile));
-            const double flops = 2.0 * (double)N * (double)N * (double)N;
+            const int64_t nb = N / kGemmTile;
+            const bool sym = !getenv("GSPARSE_XER_FULL");
+            const bool dbg = getenv("GSPARSE_XER_DEBUG") != nullptr;
+            const unsigned gg = (unsigned)(sym ? nb * (nb + 1) / 2 : nb * nb);
+            // flops one launch executes (the symmetric form runs nb(nb+1)/2 of nb^2 tiles)
+            const double flops = 2.0 * kGemmTile * kGemmTile * (double)N * (double)gg;
+            // algorithmic bytes of S = M X: X row gathers per entry + X_i + S_i per row
+            const double sbytes = 8.0 * (double)N * (double)(nnz + 2 * N);
             double prev = 1e300;
             for (int it = 0; it < 256; ++it) {
                 hipEvent_t t0 = prof_begin(c);
-                k_dgemm<<<gg, 256, 0, st>>>(N, M, X, 1.0, 0.0, nullptr, T);  // T = M X
-                prof_end(c, t0, "exact_er_dgemm", flops);
-                GS_HIP(hipMemsetAsync(mx + 1, 0, 8, st));
-                k_er_resid<<<grid_for(N * N, 256, 16384), 256, 0, st>>>(N, T, mx + 1);
-                unsigned long long rb = 0;
-                GS_HIP(hipMemcpyAsync(&rb, mx + 1, 8, hipMemcpyDeviceToHost, st));
+                k_er_spmm<<<(unsigned)sblocks, 256, 0, st>>>(n, N, ip, ix, dd, flag, X, S, rpart);
+                prof_end(c, t0, "exact_er_spmm", sbytes);
+                k_er_resid_fin<<<1, 256, 0, st>>>(rpart, sblocks, rpart + sblocks);
+                double res = 0.0;
+                GS_HIP(hipMemcpyAsync(&res, rpart + sblocks, 8, hipMemcpyDeviceToHost, st));
                 GS_HIP(hipStreamSynchronize(st));
-                double res;
-                memcpy(&res, &rb, 8);
                 it_done = it;
+                if (dbg) fprintf(stderr, "[gs_exact_er] it=%d residual=%.6e\n", it, res);
+                GS_CHECK(std::isfinite(res), GS_EHIP, "Newton-Schulz diverged at step %d", it);
                 // converged, or rounding has taken over: in the quadratic phase each
                 // step squares the residual, at the rounding floor it stalls
-                if (res < 1e-13 || (prev < 1e-3 && res > 0.5 * prev)) break;
+                if (res < 1e-14 * (double)N || (prev < 1e-2 && res > 0.5 * prev)) break;
+                GS_CHECK(it < 255, GS_EHIP, "Newton-Schulz did not converge (residual %g)", res);
                 prev = res;
                 t0 = prof_begin(c);
-                k_dgemm<<<gg, 256, 0, st>>>(N, X, T, -1.0, 2.0, X, X2);  // X2 = 2X - X T
+                if (sym)  // X2 = 2X - X S
+                    k_dgemm<true><<<gg, 256, 0, st>>>(N, X, S, -1.0, 2.0, X, X2);
+                else
+                    k_dgemm<false><<<gg, 256, 0, st>>>(N, X, S, -1.0, 2.0, X, X2);
                 prof_end(c, t0, "exact_er_dgemm", flops);
                 std::swap(X, X2);
-                GS_CHECK(it < 255, GS_EHIP, "Newton-Schulz did not converge (residual %g)", res);
             }
             if (nnz)
                 k_er_exact_scores<<<grid_for(nnz, 256, 8192), 256, 0, st>>>(
-                    N, g.rows.as<int32_t>(), g.indices.as<int32_t>(), nnz, X, dout);
+                    N, g.rows.as<int32_t>(), ix, nnz, flag, X, dout);
             GS_HIP(hipGetLastError());
         }
         finish_out(c, out, dout, sizeof(double) * nnz, loc);
