@@ -17,7 +17,8 @@ scores stay bit-identical to N=1).
 
 Other workloads (not the default line): --workload rmat (Jaccard-T on
 Graph500 R-MAT, configs[3]; --scale 22 by default), arxiv (configs[2]),
-backbone (configs[4]).
+backbone (configs[4]), exact_er (the dense exact scorer, Cora size by
+default, --xer-n for a Roman-like graph of that size; replicas at N > 1).
 
 Prints ONE JSON line (rank 0) with roofline (dominant kernel, HIP events on
 the library's stream) and cpu_baseline (the oracle's NumPy/SciPy restatement
@@ -39,6 +40,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# MI355X dense fp64 matrix peak as AMD publishes it (the microarchitecture guide lists
+# no fp64 figure); a register-only v_mfma_f64_16x16x4_f64 loop sustains 49-50 on the
+# box (tools/mfma_f64_peak.hip, profiles/r01j_mfma_f64_peak.log).
+FP64_MFMA_PEAK_TFS = 78.6
 
 
 # profiler name -> kernel symbol prefix in the rocprofv3 summaries; "jaccard"
@@ -288,16 +293,143 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
         dist.destroy_process_group()
 
 
+def cpu_baseline_exact_er(indptr, indices, data, n, max_n=4000):
+    """The reference's calculate_effective_resistance_scores (metrics.py:124-175:
+    dense pinv of L + 1e-10 I by SVD) restated in NumPy (oracle.exact_er,
+    lifted=False, bit-identical to the reference's golden vectors) on this graph,
+    or -- above max_n nodes -- on its first max_n-node induced subgraph with the
+    time scaled by (n / max_n)^3."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import scipy.sparse as sp
+
+    import gsparse_oracle as O
+
+    try:
+        from threadpoolctl import threadpool_info
+
+        cores = max(int(i.get("num_threads", 1)) for i in threadpool_info()
+                    if i.get("user_api") == "blas")
+    except Exception:
+        cores = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    m = min(n, max_n)
+    a = sp.csr_matrix((data, indices, indptr), shape=(n, n))[:m, :m].tocsr()
+    t0 = time.perf_counter()
+    O.exact_er(a.indptr, a.indices, a.data, m, lifted=False)
+    t = time.perf_counter() - t0
+    total = t * (n / m) ** 3
+    what = "this graph" if m == n else f"the first {m} nodes' subgraph, x(n/{m})^3"
+    return {"value": float(len(indices) / total), "unit": "scored edges/s", "cores": cores,
+            "kind": "port",
+            "sample": f"NumPy pinv(L + 1e-10 I) as metrics.py:159-173 on {what} "
+                      f"({t:.2f}s measured, {total:.1f}s for the graph); BLAS threads={cores}"}
+
+
+def bench_exact_er(args, world, rank, local_rank, dev, dist):
+    """calculate_effective_resistance_scores (metrics.py:124-175), the exact
+    (dense) scorer the reference runs on small graphs: default Cora-size
+    (Chung-Lu stand-in, n=2,708 / 5,278 edges, configs[0]'s graph size), or a
+    Roman-like graph of --xer-n nodes.  One step = gs_exact_er end to end
+    (components, grounding, Newton-Schulz on fp64 MFMA, per-edge read-out).
+    Replicas only: every rank scores its own copy (the dense inverse does not
+    shard without an exchange of X every step)."""
+    from gsparse import graphs
+    from gsparse._lib import Context
+    from gsparse.engine import Engine
+    from gsparse.metrics import _prepare
+
+    import scipy.sparse as sp
+
+    if args.xer_n:
+        n = args.xer_n
+        ei = graphs.roman_like(n=n, m=int(n * 32_927 / 22_662), seed=0)
+        wl = f"exact ER, Roman-like n={n}"
+    else:
+        n = 2_708
+        ei = graphs.chung_lu()
+        wl = "exact ER, Cora-size Chung-Lu (n=2,708, 5,278 undirected edges)"
+    A = sp.csr_matrix((np.ones(ei.shape[1]), (ei[0], ei[1])), shape=(n, n))
+    A.sum_duplicates()
+    a, _ = _prepare(A)
+    ctx = Context(local_rank)
+    ctx.set_graph_csr(n, a.indptr, a.indices, a.data)
+    eng = Engine(ctx)
+    E = int(a.nnz)
+    out = torch.empty(E, dtype=torch.float64, device=dev)
+
+    def step():
+        eng.exact_er(out=out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ctx.profile(True)
+    ctx.profile_reset()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        if dist.get_backend() != "nccl":
+            t = t.cpu()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    roofline = None
+    if prof and "exact_er_dgemm" in prof:
+        p = prof["exact_er_dgemm"]
+        avg_ms = p["ms"] / p["launches"]
+        fl = p["bytes"] / p["launches"]  # executed flops per launch
+        achieved = fl / (avg_ms * 1e-3) / 1e12
+        roofline = {"kernel": "k_dgemm<true,64>", "bound": "mfma", "achieved": round(achieved, 2),
+                    "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": round(achieved / FP64_MFMA_PEAK_TFS, 4), "traffic": None,
+                    "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": fl,
+                    "launches": p["launches"], "newton_schulz_steps": eng.exact_er_iterations}
+        if "exact_er_spmm" in prof:
+            q = prof["exact_er_spmm"]
+            qa = q["bytes"] / q["ms"] * 1e-6
+            roofline["spmm"] = {"bound": "hbm", "achieved": round(qa, 1), "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": round(qa / HBM_PEAK_GBS, 4),
+                                "avg_launch_ms": round(q["ms"] / q["launches"], 4)}
+    result = {
+        "metric": "scored edges/sec (exact effective resistance)",
+        "value": round(world * E * args.steps / elapsed, 1),
+        "unit": "scored edges/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (stand-in graph of the config's size; datasets are not downloadable here)",
+        "config": {"workload": wl, "n": n, "E": E,
+                   "parallelism": f"{world} replicas" if world > 1 else "1 GPU"},
+        "roofline": roofline,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_exact_er(a.indptr, a.indices, a.data, n)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="roman", choices=["roman", "rmat", "arxiv", "backbone"])
+    ap.add_argument("--workload", default="roman", choices=["roman", "rmat", "arxiv", "backbone", "exact_er"])
     ap.add_argument("--scale", type=int, default=22, help="R-MAT scale for --workload rmat")
     ap.add_argument("--bb-graph", default="rmat", choices=["rmat", "roman"],
                     help="graph of --workload backbone (R-MAT at --bb-scale, or Roman-like)")
     ap.add_argument("--bb-scale", type=int, default=18)
+    ap.add_argument("--xer-n", type=int, default=0,
+                    help="--workload exact_er on a Roman-like graph of this many nodes (0: Cora size)")
     ap.add_argument("--blas-threads", type=int, default=8,
                     help="OpenBLAS ddot order to reproduce (reference run with this many threads)")
     ap.add_argument("--rng", default=os.environ.get("GSPARSE_ER_RNG", "device"),
@@ -329,6 +461,8 @@ def main():
 
     if args.workload == "backbone":
         return bench_backbone(args, world, rank, local_rank, dev, dist)
+    if args.workload == "exact_er":
+        return bench_exact_er(args, world, rank, local_rank, dev, dist)
 
     t_gen = time.perf_counter()
     if args.workload == "roman":

@@ -22,8 +22,8 @@
 
 namespace gs {
 
-static constexpr int kGemmTile = 64;  // 64x64 output tile per 256-thread workgroup
-static constexpr int kGemmK = 16;     // K slice staged in LDS
+static constexpr int kGemmPad = 64;  // N is padded to a multiple of this
+static constexpr int kGemmK = 16;    // K slice staged in LDS
 
 // Workgroup -> output tile.  Dispatch deals consecutive workgroup ids round-robin
 // over the 8 XCDs; regroup so each XCD walks a contiguous run of tiles (shared
@@ -48,59 +48,80 @@ __device__ __forceinline__ void gemm_tile(int nb, int &bi, int &bj) {
     bj = r + (t - (r * nb - r * (r - 1) / 2));
 }
 
-// C = alpha * A * B + beta * Cin  (N x N row-major, N a multiple of 64, fp64).
-// SYM: the product is known symmetric (A, B, Cin polynomials in one symmetric
-// matrix): half the tiles, each written to both triangles.
-template <bool SYM>
+// C = alpha * A * B + beta * Cin  (N x N row-major, N a multiple of TM, fp64).
+// TM x TM output tile per 256-thread workgroup, four waves in 2x2, each wave
+// (TM/2)^2 as (TM/32)^2 v_mfma_f64_16x16x4_f64 tiles.  K advances 16 at a time
+// through LDS; the next slice is loaded into registers (16-byte loads) while
+// the current one feeds the MFMAs.  SYM: the product is symmetric (X (M X) with
+// X, M symmetric): upper-triangle tiles only, each written to both triangles.
+template <bool SYM, int TM>
 __global__ void __launch_bounds__(256) k_dgemm(int64_t N, const double *__restrict__ A,
                                                const double *__restrict__ B, double alpha,
                                                double beta, const double *__restrict__ Cin,
                                                double *__restrict__ C) {
-    __shared__ double As[kGemmTile][kGemmK + 1];
-    __shared__ double Bs[kGemmK][kGemmTile + 1];
+    constexpr int FT = TM / 32;          // MFMA tiles per wave per dimension
+    constexpr int LA = TM * kGemmK / 512;  // 16-byte loads per thread per operand
+    __shared__ double As[TM][kGemmK + 2];
+    __shared__ double Bs[kGemmK][TM + 2];
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    typedef double d4 __attribute__((ext_vector_type(4)));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int bi, bj;
-    gemm_tile<SYM>((int)(N / kGemmTile), bi, bj);
-    const int64_t r0 = (int64_t)bi * kGemmTile, c0 = (int64_t)bj * kGemmTile;
-    const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;  // the wave's 32x32 quadrant
-    typedef double d4 __attribute__((ext_vector_type(4)));
-    d4 acc[2][2];
+    gemm_tile<SYM>((int)(N / TM), bi, bj);
+    const int64_t r0 = (int64_t)bi * TM, c0 = (int64_t)bj * TM;
+    const int wr = (wave >> 1) * (TM / 2), wc = (wave & 1) * (TM / 2);
+    d4 acc[FT][FT];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FT; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
-    for (int64_t k0 = 0; k0 < N; k0 += kGemmK) {
-        // stage A[r0..+64][k0..+16] and B[k0..+16][c0..+64]: 4 doubles per thread each
+        for (int j = 0; j < FT; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+    d2 ra[LA], rb[LA];
+    auto load = [&](int64_t k0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = tid + q * 256;
-            const int ar = e / kGemmK, ac = e % kGemmK;
-            As[ar][ac] = A[(r0 + ar) * N + k0 + ac];
-            const int br = e / kGemmTile, bc = e % kGemmTile;
-            Bs[br][bc] = B[(k0 + br) * N + c0 + bc];
+        for (int q = 0; q < LA; ++q) {
+            const int e = tid + q * 256;  // d2 index within the slice
+            const int ar = e / (kGemmK / 2), ac = (e % (kGemmK / 2)) * 2;
+            ra[q] = *(const d2 *)(A + (r0 + ar) * N + k0 + ac);
+            const int br = e / (TM / 2), bc = (e % (TM / 2)) * 2;
+            rb[q] = *(const d2 *)(B + (k0 + br) * N + c0 + bc);
         }
+    };
+    auto stage = [&]() {
+#pragma unroll
+        for (int q = 0; q < LA; ++q) {
+            const int e = tid + q * 256;
+            const int ar = e / (kGemmK / 2), ac = (e % (kGemmK / 2)) * 2;
+            *(d2 *)&As[ar][ac] = ra[q];
+            const int br = e / (TM / 2), bc = (e % (TM / 2)) * 2;
+            *(d2 *)&Bs[br][bc] = rb[q];
+        }
+    };
+    load(0);
+    for (int64_t k0 = 0; k0 < N; k0 += kGemmK) {
+        stage();
         __syncthreads();
+        if (k0 + kGemmK < N) load(k0 + kGemmK);
 #pragma unroll
         for (int s = 0; s < kGemmK / 4; ++s) {
             const int kk = s * 4 + (lane >> 4);
-            double a[2], b[2];
+            double a[FT], b[FT];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) a[i] = As[wr + i * 16 + (lane & 15)][kk];
+            for (int i = 0; i < FT; ++i) a[i] = As[wr + i * 16 + (lane & 15)][kk];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) b[j] = Bs[kk][wc + j * 16 + (lane & 15)];
+            for (int j = 0; j < FT; ++j) b[j] = Bs[kk][wc + j * 16 + (lane & 15)];
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < FT; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
+                for (int j = 0; j < FT; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
         }
         __syncthreads();
     }
     // C/D map of the f64 16x16x4 form: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FT; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < FT; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int64_t row = r0 + wr + i * 16 + (lane >> 4) + 4 * r;
@@ -298,7 +319,7 @@ extern "C" int gs_exact_er(gs_ctx *c, double *out, int loc, int32_t *iterations)
         GS_HIP(hipSetDevice(c->device));
         hipStream_t st = c->stream;
         const int64_t n = g.n, nnz = g.nnz;
-        const int64_t N = ((n + kGemmTile - 1) / kGemmTile) * kGemmTile;
+        const int64_t N = ((n + kGemmPad - 1) / kGemmPad) * kGemmPad;
         double *dout = (double *)out_device(c, c->outbuf, out, sizeof(double) * (nnz ? nnz : 1), loc);
         int32_t it_done = 0;
         if (n > 0) {
@@ -344,12 +365,16 @@ extern "C" int gs_exact_er(gs_ctx *c, double *out, int loc, int32_t *iterations)
             const int64_t sblocks = N * ((N + 255) / 256);
             auto *rpart = (double *)c->buf("xer_resid").ensure(8 * (sblocks + 1));
             k_er_xinit<<<grid_for(N * N, 256, 65536), 256, 0, st>>>(N, mx, X);
-            const int64_t nb = N / kGemmTile;
             const bool sym = !getenv("GSPARSE_XER_FULL");
             const bool dbg = getenv("GSPARSE_XER_DEBUG") != nullptr;
+            // 64-wide tiles (4 waves/SIMD); the 128-wide form holds 1 wave/SIMD and
+            // measured slower at every size (DESIGN.md §Exact ER), kept behind the knob
+            int tm = 64;
+            if (const char *e = getenv("GSPARSE_XER_TILE")) tm = (atoi(e) == 128 && N % 128 == 0) ? 128 : 64;
+            const int64_t nb = N / tm;
             const unsigned gg = (unsigned)(sym ? nb * (nb + 1) / 2 : nb * nb);
             // flops one launch executes (the symmetric form runs nb(nb+1)/2 of nb^2 tiles)
-            const double flops = 2.0 * kGemmTile * kGemmTile * (double)N * (double)gg;
+            const double flops = 2.0 * tm * tm * (double)N * (double)gg;
             // algorithmic bytes of S = M X: X row gathers per entry + X_i + S_i per row
             const double sbytes = 8.0 * (double)N * (double)(nnz + 2 * N);
             double prev = 1e300;
@@ -370,10 +395,15 @@ extern "C" int gs_exact_er(gs_ctx *c, double *out, int loc, int32_t *iterations)
                 GS_CHECK(it < 255, GS_EHIP, "Newton-Schulz did not converge (residual %g)", res);
                 prev = res;
                 t0 = prof_begin(c);
-                if (sym)  // X2 = 2X - X S
-                    k_dgemm<true><<<gg, 256, 0, st>>>(N, X, S, -1.0, 2.0, X, X2);
+                // X2 = 2X - X S
+                if (sym && tm == 128)
+                    k_dgemm<true, 128><<<gg, 256, 0, st>>>(N, X, S, -1.0, 2.0, X, X2);
+                else if (sym)
+                    k_dgemm<true, 64><<<gg, 256, 0, st>>>(N, X, S, -1.0, 2.0, X, X2);
+                else if (tm == 128)
+                    k_dgemm<false, 128><<<gg, 256, 0, st>>>(N, X, S, -1.0, 2.0, X, X2);
                 else
-                    k_dgemm<false><<<gg, 256, 0, st>>>(N, X, S, -1.0, 2.0, X, X2);
+                    k_dgemm<false, 64><<<gg, 256, 0, st>>>(N, X, S, -1.0, 2.0, X, X2);
                 prof_end(c, t0, "exact_er_dgemm", flops);
                 std::swap(X, X2);
             }
