@@ -48,7 +48,8 @@ FP64_MFMA_PEAK_TFS = 78.6
 
 # profiler name -> kernel symbol prefix in the rocprofv3 summaries; "jaccard"
 # is a pipeline of kernels (plan, light, hash classes, bitmap), summed per call
-PMC_KERNEL = {"cg_pq": "gs::k_cg_pq<false", "cg_upd": "gs::k_cg_upd<", "jaccard": "gs::k_jac_",
+PMC_KERNEL = {"cg_res": "gs::k_cg_resident<", "cg_pq": "gs::k_cg_pq<false", "cg_upd": "gs::k_cg_upd<",
+              "jaccard": "gs::k_jac_",
               "cg_p": "gs::k_cg_p", "cg_spmv": "gs::k_spmv<"}
 
 

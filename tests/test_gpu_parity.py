@@ -59,15 +59,59 @@ def test_approx_er_bit_exact(gs, name):
     assert bits_equal(er, ref), float(np.max(np.abs(er - ref) / np.abs(ref)))
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4"])
 @pytest.mark.parametrize("name", ["karate_csr", "rmat10", "directed_dup", "roman2000"])
 def test_approx_er_all_cg_modes(gs, name, mode, monkeypatch):
     """q recomputed in the update kernel (0), stored by the fused p/q kernel (1),
-    or split p stream + SpMV (2) -- the same bits in every mode."""
+    split p stream + SpMV (2, 3), or the resident per-column solver (4) -- the
+    same bits in every mode."""
     monkeypatch.setenv("GSPARSE_CG_MODE", mode)
     g = load_golden(name)
     sp_, _ = make(gs, g, with_x=False)
     assert bits_equal(sp_._engine.approx_er(blas_threads=1), g["scores_approx_er"])
+
+
+@pytest.fixture(scope="module")
+def chunked_er():
+    """n > 10000, so OpenBLAS splits every ddot into T thread chunks; a short
+    maxiter keeps the oracle's CG (oracle.c) to seconds."""
+    from gsparse import graphs
+
+    n = 12000
+    ei = graphs.roman_like(n, 17500, seed=3)
+    # the same graph with every 7th edge doubled: multiplicity-2 entries, so the
+    # resident solver's unit-weight SELL form does not apply
+    dup = np.concatenate([ei, ei[:, ::7]], axis=1)
+    out = {}
+    for gname, e in (("unit", ei), ("dup", dup)):
+        ip, ix, d = O.canonical_csr(e, n)
+        out[gname] = (e, {t: O.approx_er(ip, ix, d, n, epsilon=0.9, max_cg_iters=60, impl="c",
+                                         blas_threads=t) for t in (3, 8)})
+    return n, out
+
+
+@pytest.mark.parametrize("env", [{"GSPARSE_CG_MODE": "0"}, {"GSPARSE_CG_MODE": "1"},
+                                 {"GSPARSE_CG_MODE": "3"}, {"GSPARSE_CG_MODE": "4"},
+                                 {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_ELL": "1"},
+                                 {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_QLDS": "0"},
+                                 {"GSPARSE_CG_MODE": "4", "GSPARSE_CG_SLOTS": "7"},
+                                 {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_UNIT": "0"},
+                                 {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_UNIT": "0",
+                                  "GSPARSE_RES_ELL": "1"}],
+                         ids=["m0", "m1", "m3", "m4", "m4-ell", "m4-q-global", "m4-7slots",
+                              "m4-weighted-sell", "m4-weighted-ell"])
+@pytest.mark.parametrize("threads", [3, 8])
+@pytest.mark.parametrize("graph", ["unit", "dup"])
+def test_approx_er_blas_chunks_vs_oracle(gs, chunked_er, graph, threads, env, monkeypatch):
+    """T-chunk ddot order (T = 3, 8) in every CG mode, bit-identical to the oracle."""
+    for k_, v in env.items():
+        monkeypatch.setenv(k_, v)
+    n, graphs_ = chunked_er
+    ei, ref = graphs_[graph]
+    data = gs.Data(edge_index=torch.from_numpy(ei), num_nodes=n)
+    sp_ = gs.GraphSparsifier(data, "cpu")
+    er = sp_._engine.approx_er(epsilon=0.9, max_cg_iters=60, blas_threads=threads)
+    assert bits_equal(er, ref[threads])
 
 
 def test_approx_er_roman_full_bit_exact(gs):
