@@ -1744,10 +1744,15 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         auto *dch = (int64_t *)c->buf("er_chunks").ensure(sizeof(hch));
         GS_HIP(hipMemcpyAsync(dch, hch, sizeof(hch), hipMemcpyHostToDevice, c->stream));
         const int64_t *ca = dch, *cl = dch + kMaxChunks;
-        // algorithmic bytes: pq reads x, p, r and writes x, p (first iteration: r in, p out)
-        // (+ q written when stored); upd reads p (or q), r and writes r
+        // algorithmic bytes, SURVEY 8(d) B_ER: per column and iteration 8 (nnz(L_reg) + 10 n),
+        // i.e. one 8-B p read per L_reg entry (the SpMV) + the vector streams.  Attributed
+        // to the kernel that does each part: pq reads x, p, r and writes x, p (first
+        // iteration: r in, p out) and performs the SpMV (+ q written when stored); upd
+        // reads p (or q), r and writes r (its q recompute is not counted again)
         const double qb = storeq ? 8.0 : 0.0;
-        const double bytes_pq = (40.0 + qb) * n * ncols, bytes_pq0 = (16.0 + qb) * n * ncols,
+        const double lnz = (double)er.lnnz;
+        const double bytes_pq = ((40.0 + qb) * n + 8.0 * lnz) * ncols,
+                     bytes_pq0 = ((16.0 + qb) * n + 8.0 * lnz) * ncols,
                      bytes_upd = 24.0 * n * ncols;
         const int64_t *lp = er.lp.as<int64_t>();
         const int32_t *li = er.li.as<int32_t>();
@@ -1848,15 +1853,15 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             GS_HIP(hipMemcpyAsync(er.iters.ptr, cp.iters, sizeof(int32_t) * k, hipMemcpyDeviceToDevice,
                                   c->stream));
             if (prof_rec) {
-                // algorithmic bytes: b in + x out per column, 64 B per row and iteration
-                // (p update: r, p, x in, p, x out; r update: r, q in, r out) -- as the batched modes
+                // algorithmic bytes (SURVEY 8(d) B_ER): 8 (nnz(L_reg) + 10 n) per column and
+                // iteration, + b in and x out per column
                 std::vector<int32_t> hit((size_t)ncols);
                 GS_HIP(hipMemcpyAsync(hit.data(), cp.iters + col0, sizeof(int32_t) * ncols,
                                       hipMemcpyDeviceToHost, c->stream));
                 GS_HIP(hipStreamSynchronize(c->stream));
                 double its = 0.0;
                 for (int32_t v : hit) its += v;
-                c->pending.back().bytes = 64.0 * n * its + 16.0 * n * ncols;
+                c->pending.back().bytes = 8.0 * ((double)er.lnnz + 10.0 * n) * its + 16.0 * n * ncols;
             }
             GS_HIP(hipStreamSynchronize(c->stream));
             if (rprof) {
@@ -1923,7 +1928,7 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
                 t0 = prof_begin(c);
                 if (mode == 2) {
                     if (cpl == 2) GS_Q(2); else GS_Q(1);
-                    prof_end(c, t0, "cg_q", 16.0 * n * ncols);
+                    prof_end(c, t0, "cg_q", (24.0 * n + 8.0 * lnz) * ncols);
                 } else {
                     // 4 rows per wave, 128 columns: best of {1..64} x {64, 128} on ogbn-arxiv size
                     const int64_t rpw = 4;
@@ -1936,7 +1941,7 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
                         k_spmv<2><<<sg, 256, 0, c->stream>>>(GS, rpw, ntiles, lp, li, lv, Pnew, Qfull, cp.active);
                     else
                         k_spmv<1><<<sg, 256, 0, c->stream>>>(GS, rpw, ntiles, lp, li, lv, Pnew, Qfull, cp.active);
-                    prof_end(c, t0, "cg_spmv", 8.0 * n * ncols);
+                    prof_end(c, t0, "cg_spmv", (8.0 * n + 8.0 * lnz) * ncols);
                     t0 = prof_begin(c);
                     if (cpl == 2) k_dot_acc<2, 4><<<grid, block, 0, c->stream>>>(G, ch, Pnew, Qfull, acc);
                     else k_dot_acc<1, 4><<<grid, block, 0, c->stream>>>(G, ch, Pnew, Qfull, acc);
