@@ -114,6 +114,29 @@ def test_approx_er_blas_chunks_vs_oracle(gs, chunked_er, graph, threads, env, mo
     assert bits_equal(er, ref[threads])
 
 
+@pytest.mark.parametrize("mode", ["0", "4"])
+def test_er_column_blocks_in_every_mode(gs, chunked_er, mode, monkeypatch):
+    """A rank's column block [col0, col1) (the N-GPU split) solved alone, in the
+    batched and the resident solver: the blocks' partial sums, added along the
+    pairwise tree, equal the whole -- and the whole equals the oracle."""
+    monkeypatch.setenv("GSPARSE_CG_MODE", mode)
+    n, graphs_ = chunked_er
+    ei, ref = graphs_["unit"]
+    sp_ = gs.GraphSparsifier(gs.Data(edge_index=torch.from_numpy(ei), num_nodes=n), "cpu")
+    e = sp_._engine
+    k = gs.engine.jl_dim(n, 0.9)
+    e.er_prepare(k)
+    e.er_project_device(np.random.default_rng(42), k)
+    b = gs.engine.er_split(k, 2)
+    sums = []
+    for i in range(2):  # each block solved on its own, as one rank would
+        e.er_solve(int(b[i]), int(b[i + 1]), 60, 1e-6, 8)
+        sums.append(e.er_scores(int(b[i]), int(b[i + 1]), finalize=False))
+    tot = 0.0 + (sums[0] + sums[1])
+    tot = np.maximum(np.nan_to_num(tot, nan=1e-10, posinf=1e-10, neginf=1e-10), 1e-10)
+    assert bits_equal(tot, ref[8])
+
+
 def test_approx_er_roman_full_bit_exact(gs):
     """configs[1] size (n=22,662, E=65,854, k=2,674, 500 CG iterations per column)."""
     g = load_golden("roman_full")
