@@ -1148,6 +1148,7 @@ struct ResArgs {
     const double *eval;      // weight (nullptr in the unit-weight form)
     int64_t lde;
     int64_t ql;              // rows of q mirrored in LDS (dynamic shared memory)
+    int64_t nstab;           // SELL slices whose (offset, width) are staged in LDS after q (0: none)
     long long *prof;         // optional: workgroup 0's phase times (wall clock ticks)
 };
 
@@ -1166,7 +1167,8 @@ __device__ __forceinline__ double wave_uniform(double v) {
 // (SciPy csr_matvec).  The first W entries of each row are loaded at once
 // (then all their gathers), wider rows finish in a tail loop.
 template <int RB, int W, bool UNIT>
-__device__ __forceinline__ void res_spmv(const ResArgs &A, const double *p, double *q, double *sq, int64_t ql) {
+__device__ __forceinline__ void res_spmv(const ResArgs &A, const double *p, double *q, double *sq, int64_t ql,
+                                         const int2 *stab) {
     const int64_t n = A.n;
     const int64_t ntile = (n + 63) >> 6;  // 64-row tiles, one per wave-trip row
     for (int64_t t0 = threadIdx.x >> 6; t0 < ntile; t0 += (int64_t)kResWaves * RB) {
@@ -1181,8 +1183,15 @@ __device__ __forceinline__ void res_spmv(const ResArgs &A, const double *p, doub
             ok[i] = t < ntile && rw < n;
             row[i] = ok[i] ? rw : 0;
             const int64_t b = row[i] / kSell;
-            o[i] = A.soff[b] + row[i] % kSell;
-            const int32_t wb = A.swid[b];
+            int32_t wb;
+            if (stab) {  // slice table staged in LDS: no dependent global load
+                const int2 t = stab[b];
+                o[i] = (int64_t)t.x + row[i] % kSell;
+                wb = t.y;
+            } else {
+                o[i] = A.soff[b] + row[i] % kSell;
+                wb = A.swid[b];
+            }
             w[i] = ok[i] ? wb : 0;
             wmax = w[i] > wmax ? w[i] : wmax;
             dg[i] = UNIT ? A.sdiag[row[i]] : 0.0;
@@ -1290,10 +1299,14 @@ template <int RB, int W, int RC, bool UNIT, int EW>
 __global__ void __launch_bounds__(kResThreads) k_cg_resident(ResArgs A, ChunkArg ch) {
     __shared__ double s_acc[kMaxChunks * 32];
     __shared__ double s_bc;
-    extern __shared__ double sq[];  // q of rows < ql (LDS mirror of the q slot)
+    extern __shared__ double sq[];  // q of rows < ql (LDS mirror of the q slot), then the slice table
     const int tid = threadIdx.x;
     const int nchains = ch.count * 32;
     const int64_t n = A.n, ql = A.ql;
+    int2 *stab = reinterpret_cast<int2 *>(sq + ql);
+    for (int64_t b = tid; b < A.nstab; b += kResThreads)
+        stab[b] = make_int2((int)A.soff[b], A.swid[b]);
+    __syncthreads();
     double *r = A.slots + (int64_t)blockIdx.x * 3 * A.ldn;
     double *p = r + A.ldn;
     double *q = p + A.ldn;
@@ -1396,7 +1409,7 @@ __global__ void __launch_bounds__(kResThreads) k_cg_resident(ResArgs A, ChunkArg
             __syncthreads();
             lap(0);
             if (EW) res_spmv_ell<EW <= 8 ? 2 : 1, EW, UNIT>(A, p, q, sq, ql);
-            else res_spmv<RB, W, UNIT>(A, p, q, sq, ql);
+            else res_spmv<RB, W, UNIT>(A, p, q, sq, ql, A.nstab ? stab : nullptr);
             __syncthreads();
             lap(1);
             chain_dot(p, q, true);
@@ -1818,12 +1831,18 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             if (getenv("GSPARSE_RES_PROF"))
                 rprof = (long long *)c->buf("er_res_prof").ensure(8 * sizeof(long long));
             ResArgs ra{n, er.ld, ldn, col0, ncols, lp, li, lv, Rr, Xc, sl, ca, cl, maxiter, rtol,
-                       cp.iters, soff, swid, scol, sval, sdiag, ecol, evalp, lde, 0, rprof};
+                       cp.iters, soff, swid, scol, sval, sdiag, ecol, evalp, lde, 0, 0, rprof};
             // q mirror in LDS: what the 160 KiB leave after the static 16 KiB
-            int64_t qlmax = (140 * 1024) / 8;
+            // dynamic LDS (140 KiB next to the 16 KiB chain table): the SELL slice table
+            // (8 B per 16 rows, when the offsets fit int32) and a mirror of q's first rows
+            size_t lds = 140 * 1024;
+            ra.nstab = (sent < (int64_t)1 << 31 && (size_t)nbk * 8 <= lds / 4) ? nbk : 0;
+            if (const char *e = getenv("GSPARSE_RES_STAB")) if (atoi(e) == 0) ra.nstab = 0;
+            lds -= (size_t)ra.nstab * 8;
+            int64_t qlmax = (int64_t)(lds / 8);
             if (const char *e = getenv("GSPARSE_RES_QLDS")) qlmax = atoi(e) ? qlmax : 0;
             ra.ql = n < qlmax ? n : qlmax;
-            const size_t dyn = sizeof(double) * (size_t)(ra.ql > 0 ? ra.ql : 1);
+            const size_t dyn = sizeof(double) * (size_t)ra.ql + 8 * (size_t)ra.nstab + 8;
             hipEvent_t t0 = prof_begin(c);
 #define GS_RES(B, W, C, U, E)                                                                  \
     do {                                                                                        \
@@ -1831,7 +1850,18 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));     \
         k_cg_resident<B, W, C, U, E><<<(unsigned)slots, kResThreads, dyn, c->stream>>>(ra, ch); \
     } while (0)
-#define GS_RES_U(E) do { if (unit) GS_RES(4, 4, 16, true, E); else GS_RES(4, 4, 16, false, E); } while (0)
+            // SpMV rows per thread-trip and entries loaded at once: 2 x 8 (Roman: 36 us per
+            // column-iteration vs 40 us for 4 x 4, whose rows wider than 4 take the tail loop)
+            int rbw = 28;
+            if (const char *e = getenv("GSPARSE_RES_RBW")) rbw = atoi(e) == 44 ? 44 : 28;
+#define GS_RES_U(E)                                                  \
+    do {                                                             \
+        if (rbw == 28) {                                             \
+            if (unit) GS_RES(2, 8, 16, true, E); else GS_RES(2, 8, 16, false, E); \
+        } else {                                                     \
+            if (unit) GS_RES(4, 4, 16, true, E); else GS_RES(4, 4, 16, false, E); \
+        }                                                            \
+    } while (0)
             if (n) {
                 if (ew == 4) GS_RES_U(4);
                 else if (ew == 8) GS_RES_U(8);
