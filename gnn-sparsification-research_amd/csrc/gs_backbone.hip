@@ -175,28 +175,86 @@ __device__ void bb_search(const int64_t *__restrict__ gp, const int32_t *__restr
         const double wmax = s_wmax;
         for (int f = threadIdx.x; f < fc; f += blockDim.x) qflag[cur[f]] = 0;
         __syncthreads();
-        for (int f = threadIdx.x; f < fc; f += blockDim.x) {
-            const int32_t x = cur[f];
-            const double dx = __longlong_as_double(
-                (long long)__hip_atomic_load(&dist[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            for (int64_t e = gp[x]; e < gp[x + 1]; ++e) {
-                ++relax;
-                const double nd = dx + gw[e];
-                if (!(nd <= wmax)) continue;
-                const int32_t y = gi[e];
-                const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
-                const unsigned long long old = atomicMin(&dist[y], nb);
-                if (nb < old) {
-                    if (old == kInfBits) {
-                        int t = atomicAdd(&s_tcount, 1);
-                        touched[t] = y;
+        // edge-parallel expansion: each wave takes 64 frontier nodes, scans their
+        // degrees, and its lanes walk the concatenated edge lists 64 at a time
+        // (coalesced, balanced across hubs and leaves); a relaxation only
+        // issues the 64-bit atomicMin after a plain load shows it improves
+        __shared__ int32_t w_pre[4][65];
+        __shared__ int64_t w_beg[4][64];
+        __shared__ double w_d[4][64];
+        const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        for (int f0 = wv * 64; f0 < fc; f0 += (int)blockDim.x) {
+            const int f = f0 + lane;
+            int deg = 0;
+            int64_t b = 0;
+            double dx = 0.0;
+            if (f < fc) {
+                const int32_t x = cur[f];
+                b = gp[x];
+                deg = (int)(gp[x + 1] - b);
+                dx = __longlong_as_double(
+                    (long long)__hip_atomic_load(&dist[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            }
+            int incl = deg;
+            for (int off = 1; off < 64; off <<= 1) {
+                const int t = __shfl_up(incl, off, 64);
+                if (lane >= off) incl += t;
+            }
+            const int total = __shfl(incl, 63, 64);
+            w_pre[wv][lane + 1] = incl;
+            if (lane == 0) w_pre[wv][0] = 0;
+            w_beg[wv][lane] = b;
+            w_d[wv][lane] = dx;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            constexpr int U = 4;  // edges per lane per trip, all loads in flight
+            for (int e0 = 0; e0 < total; e0 += 64 * U) {
+                int32_t y[U];
+                unsigned long long nb[U], cur_d[U];
+                bool go[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int e = e0 + u * 64 + lane;
+                    go[u] = e < total;
+                    const int ec = go[u] ? e : 0;
+                    int lo = 0, hi = 63;  // largest k with w_pre[k] <= ec
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (w_pre[wv][mid] <= ec) lo = mid;
+                        else hi = mid - 1;
                     }
-                    if (atomicExch(&qflag[y], 1) == 0) {
-                        int q = atomicAdd(&s_ncount, 1);
-                        nxt[q] = y;
+                    const int64_t ei = w_beg[wv][lo] + (ec - w_pre[wv][lo]);
+                    relax += go[u] ? 1 : 0;
+                    const double nd = w_d[wv][lo] + gw[ei];
+                    go[u] = go[u] && (nd <= wmax);
+                    y[u] = gi[ei];
+                    nb[u] = (unsigned long long)__double_as_longlong(nd);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    cur_d[u] = go[u] ? __hip_atomic_load(&dist[y[u]], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0ull;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (!go[u] || nb[u] >= cur_d[u]) continue;
+                    const unsigned long long old = atomicMin(&dist[y[u]], nb[u]);
+                    if (nb[u] < old) {
+                        if (old == kInfBits) {
+                            int t = atomicAdd(&s_tcount, 1);
+                            touched[t] = y[u];
+                        }
+                        if (atomicExch(&qflag[y[u]], 1) == 0) {
+                            int q = atomicAdd(&s_ncount, 1);
+                            nxt[q] = y[u];
+                        }
                     }
                 }
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -607,7 +665,9 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
             if (nsrc > 0) {
                 int64_t *sources = (int64_t *)b_sources.ensure(8 * nsrc);
                 k_bb_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(flag, pos, n, sources);
-                int64_t slabs = nsrc < 1024 ? nsrc : 1024;
+                int64_t maxslabs = 1024;
+                if (const char *e = getenv("GSPARSE_BB_SLABS")) maxslabs = atoi(e) > 0 ? atoi(e) : 1024;
+                int64_t slabs = nsrc < maxslabs ? nsrc : maxslabs;
                 // keep the per-slab working set under ~8 GB
                 int64_t cap = (int64_t)(8e9 / (24.0 * (double)(n ? n : 1)));
                 if (cap < 1) cap = 1;
