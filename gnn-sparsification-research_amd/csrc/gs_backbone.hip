@@ -179,9 +179,9 @@ __device__ void bb_search(const int64_t *__restrict__ gp, const int32_t *__restr
         // degrees, and its lanes walk the concatenated edge lists 64 at a time
         // (coalesced, balanced across hubs and leaves); a relaxation only
         // issues the 64-bit atomicMin after a plain load shows it improves
-        __shared__ int32_t w_pre[4][65];
-        __shared__ int64_t w_beg[4][64];
-        __shared__ double w_d[4][64];
+        __shared__ int32_t w_pre[16][65];  // per wave (blocks of up to 1024 threads)
+        __shared__ int64_t w_beg[16][64];
+        __shared__ double w_d[16][64];
         const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
         for (int f0 = wv * 64; f0 < fc; f0 += (int)blockDim.x) {
             const int f = f0 + lane;
@@ -288,7 +288,8 @@ __device__ void bb_block_max(double v, double *out) {
     __syncthreads();
 }
 
-__global__ void __launch_bounds__(256) k_bb_sssp(
+template <int NT>
+__global__ void __launch_bounds__(NT) k_bb_sssp(
     const int64_t *__restrict__ gp, const int32_t *__restrict__ gi, const double *__restrict__ gw,
     int64_t n, const int64_t *__restrict__ sources, int64_t nsrc, const int64_t *__restrict__ optr,
     const int64_t *__restrict__ order, const int64_t *__restrict__ dst,
@@ -665,8 +666,10 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
             if (nsrc > 0) {
                 int64_t *sources = (int64_t *)b_sources.ensure(8 * nsrc);
                 k_bb_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(flag, pos, n, sources);
-                int64_t maxslabs = 1024;
-                if (const char *e = getenv("GSPARSE_BB_SLABS")) maxslabs = atoi(e) > 0 ? atoi(e) : 1024;
+                // one 1024-thread workgroup per CU (RMAT-18: 4.1 s; 1,024 x 256 threads 5.2 s,
+                // 512 x 512 4.4 s, 128 x 1,024 5.9 s)
+                int64_t maxslabs = 256;
+                if (const char *e = getenv("GSPARSE_BB_SLABS")) maxslabs = atoi(e) > 0 ? atoi(e) : 256;
                 int64_t slabs = nsrc < maxslabs ? nsrc : maxslabs;
                 // keep the per-slab working set under ~8 GB
                 int64_t cap = (int64_t)(8e9 / (24.0 * (double)(n ? n : 1)));
@@ -679,7 +682,10 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                 k_bb_fill_u64<<<grid_for(slabs * n, 256, 65536), 256, 0, s>>>(dist, slabs * n,
                                                                                kInfBits);
                 GS_HIP(hipMemsetAsync(qflag, 0, 4 * slabs * n, s));
-                k_bb_sssp<<<(unsigned)slabs, 256, 0, s>>>(gp, gi, gw, n, sources, nsrc, optr, order,
+                int bt = 1024;
+                if (const char *e = getenv("GSPARSE_BB_THREADS")) bt = atoi(e) == 1024 ? 1024 : atoi(e) == 512 ? 512 : 256;
+                auto kfn = bt == 1024 ? k_bb_sssp<1024> : bt == 512 ? k_bb_sssp<512> : k_bb_sssp<256>;
+                kfn<<<(unsigned)slabs, bt, 0, s>>>(gp, gi, gw, n, sources, nsrc, optr, order,
                                                           ddst, dw, eps, state, dist, qflag, fr,
                                                           touched, misc + 1);
                 GS_HIP(hipGetLastError());
