@@ -49,7 +49,7 @@ FP64_MFMA_PEAK_TFS = 78.6
 # profiler name -> kernel symbol prefix in the rocprofv3 summaries; "jaccard"
 # is a pipeline of kernels (plan, light, hash classes, bitmap), summed per call
 PMC_KERNEL = {"cg_res": "gs::k_cg_resident<", "cg_pq": "gs::k_cg_pq<false", "cg_upd": "gs::k_cg_upd<",
-              "jaccard": "gs::k_jac_",
+              "jaccard": "gs::k_jac_", "metric_backbone": "gs::k_bb_",
               "cg_p": "gs::k_cg_p", "cg_spmv": "gs::k_spmv<"}
 
 
@@ -74,11 +74,13 @@ def pmc_traffic(name: str, workload: str):
     def kb(v):
         return (2.0 * v["FETCH_SIZE_KB_per_launch"] + v["WRITE_SIZE_KB_per_launch"]) * 1024.0
 
-    if name == "jaccard":
-        calls = max(1, max(v.get("launches", 1) for k, v in hits if "k_jac_plan" in k) if any(
-            "k_jac_plan" in k for k, _ in hits) else 1)
+    if name in ("jaccard", "metric_backbone"):
+        # pipelines: the kernels of one call summed (the plan / search kernel runs once per call)
+        anchor = "k_jac_plan" if name == "jaccard" else "k_bb_keep"
+        calls = max(1, max(v.get("launches", 1) for k, v in hits if anchor in k) if any(
+            anchor in k for k, _ in hits) else 1)
         b = sum(kb(v) * v.get("launches", 1) for _, v in hits) / calls
-        return b, f"{os.path.basename(files[-1])}: sum of {len(hits)} gs::k_jac_* kernels"
+        return b, f"{os.path.basename(files[-1])}: sum of {len(hits)} {pre}* kernels"
     k, v = max(hits, key=lambda kv: kv[1].get("launches", 0))
     return kb(v), f"{os.path.basename(files[-1])}: {k}"
 
@@ -275,6 +277,11 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                     "avg_launch_ms": round(avg_ms, 3), "algorithmic_bytes_per_launch": bytes_per,
                     "launches": p["launches"], "relaxations_per_launch_rank0": relax.value}
+        key = f"backbone-{args.bb_graph}" + (str(args.bb_scale) if args.bb_graph == "rmat" else "")
+        traffic, tsrc = pmc_traffic("metric_backbone", key)
+        if traffic:
+            roofline["traffic"] = round(traffic)
+            roofline["traffic_source"] = tsrc
     result = {
         "metric": "scored edges/sec (metric backbone)", "value": round(E * args.steps / elapsed, 1),
         "unit": "scored edges/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
