@@ -31,18 +31,28 @@ static int bits_for_bb(uint64_t v) {
 static constexpr uint64_t kInfBits = 0x7ff0000000000000ull;
 static constexpr int kBbLandmarkRounds = 256;  // frontier rounds per landmark search
 
+// osrc/odst: the caller's ids (which columns are s < d: metric_backbone.py:70-79
+// builds G from those); src/dst: the (possibly relabeled) ids G is built in
 __global__ void k_bb_keys(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
+                          const int64_t *__restrict__ osrc, const int64_t *__restrict__ odst,
                           const double *__restrict__ w, int64_t E, int64_t n,
                           uint64_t *__restrict__ keys, int64_t *__restrict__ idx,
                           int *__restrict__ bad) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
          i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t s = src[i], d = dst[i];
-        if (s < 0 || s >= n || d < 0 || d >= n) atomicOr(bad, 1);
+        const int64_t os = osrc[i], od = odst[i];
+        if (os < 0 || os >= n || od < 0 || od >= n) {
+            atomicOr(bad, 1);
+            keys[i] = ~0ull;
+            idx[i] = i;
+            continue;
+        }
+        const int64_t s = src[i], d = dst[i];
         double x = w[i];
         if (!(x >= 0.0)) atomicOr(bad, 2);  // negative or NaN weight
-        // undirected edges from s<d columns; others sort to the end
-        keys[i] = (s < d && s >= 0 && d < n) ? (uint64_t)s * (uint64_t)n + (uint64_t)d : ~0ull;
+        // undirected edges from s<d columns (caller's ids); others sort to the end
+        const uint64_t lo = (uint64_t)(s < d ? s : d), hi = (uint64_t)(s < d ? d : s);
+        keys[i] = os < od ? lo * (uint64_t)n + hi : ~0ull;
         idx[i] = i;
     }
 }
@@ -535,6 +545,59 @@ __global__ void k_bb_keep(const uint8_t *__restrict__ state, const int64_t *__re
 
 using namespace gs;
 
+// Node relabeling for the searches' locality: node ids ordered by descending
+// column count (hubs first, ties by id), so the labels a search touches most
+// often share cache lines.  Distances, sums and decisions do not depend on the
+// labels (every fold runs along the path from the source), only where the
+// searches' distance slabs are read.
+__global__ void k_bb_count(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
+                           int64_t E, unsigned long long *__restrict__ cnt) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        atomicAdd(&cnt[src[i]], 1ull);
+        atomicAdd(&cnt[dst[i]], 1ull);
+    }
+}
+
+// sum over columns of |src - dst| (the ids' existing locality), per-wave partials
+__global__ void k_bb_gap(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
+                         int64_t E, unsigned long long *__restrict__ sum) {
+    unsigned long long acc = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t g = src[i] - dst[i];
+        acc += (unsigned long long)(g < 0 ? -g : g);
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(sum, acc);
+}
+
+__global__ void k_bb_relabel_keys(const unsigned long long *__restrict__ cnt, int64_t n,
+                                  uint64_t *__restrict__ keys, int64_t *__restrict__ ids) {
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = cnt[x] < 0xffffffffull ? cnt[x] : 0xffffffffull;
+        keys[x] = ((0xffffffffull - c) << 32) | (uint64_t)x;
+        ids[x] = x;
+    }
+}
+
+__global__ void k_bb_perm(const int64_t *__restrict__ ids, int64_t n, int64_t *__restrict__ perm) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        perm[ids[i]] = i;
+}
+
+__global__ void k_bb_map(const int64_t *__restrict__ perm, const int64_t *__restrict__ a,
+                         const int64_t *__restrict__ b, int64_t E, int64_t *__restrict__ ma,
+                         int64_t *__restrict__ mb) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        ma[i] = perm[a[i]];
+        mb[i] = perm[b[i]];
+    }
+}
+
 extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const int64_t *src,
                                        const int64_t *dst, const double *w, int loc, double eps,
                                        int part, int nparts, uint8_t *keep, int keep_loc,
@@ -552,11 +615,56 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
         BB(src); BB(dst); BB(w); BB(keys); BB(idx); BB(ukeys); BB(uw); BB(pay); BB(gp); BB(gi);
         BB(gw); BB(okeys); BB(order); BB(optr); BB(state); BB(flag); BB(pos); BB(sources);
         BB(dist); BB(qflag); BB(fr); BB(touched); BB(misc); BB(keep); BB(lm); BB(land); BB(lcomp);
+        BB(msrc); BB(mdst); BB(perm);
 #undef BB
         const int64_t *dsrc =
             (const int64_t *)to_device(c, b_src, src, sizeof(int64_t) * E, loc);
         const int64_t *ddst =
             (const int64_t *)to_device(c, b_dst, dst, sizeof(int64_t) * E, loc);
+        const int64_t *osrc = dsrc, *odst = ddst;  // the caller's ids
+        bool relabel = E > 0 && n > 1;
+        if (const char *e = getenv("GSPARSE_BB_RELABEL")) relabel = relabel && atoi(e) != 0;
+        // only graphs whose ids carry no locality of their own (mean |u - v| above n / 64:
+        // R-MAT 0.33 n; a word chain with short chords ~2) -- relabeling a chain-ordered
+        // graph by degree would scatter it (Roman-like: 2.2 -> 3.2 ms)
+        if (relabel && !getenv("GSPARSE_BB_RELABEL")) {
+            unsigned long long *gs = (unsigned long long *)c->buf("bb_gap").ensure(8);
+            GS_HIP(hipMemsetAsync(gs, 0, 8, s));
+            k_bb_gap<<<grid_for(E, 256, 2048), 256, 0, s>>>(dsrc, ddst, E, gs);
+            unsigned long long hg = 0;
+            GS_HIP(hipMemcpyAsync(&hg, gs, 8, hipMemcpyDeviceToHost, s));
+            GS_HIP(hipStreamSynchronize(s));
+            relabel = (double)hg / (double)E > (double)n / 64.0;
+        }
+        if (relabel) {
+            // validate before indexing the counters with the raw ids
+            int *bad0 = (int *)c->buf("bb_bad0").ensure(sizeof(int));
+            GS_HIP(hipMemsetAsync(bad0, 0, sizeof(int), s));
+            uint64_t *k0 = (uint64_t *)c->buf("bb_keys").ensure(8 * E);
+            int64_t *i0 = (int64_t *)c->buf("bb_idx").ensure(8 * E);
+            k_bb_keys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, dsrc, ddst, (const double *)to_device(
+                c, c->buf("bb_w"), w, sizeof(double) * E, loc), E, n, k0, i0, bad0);
+            int hb = 0;
+            GS_HIP(hipMemcpyAsync(&hb, bad0, 4, hipMemcpyDeviceToHost, s));
+            GS_HIP(hipStreamSynchronize(s));
+            GS_CHECK(!(hb & 1), GS_EINVAL, "edge_index entry out of range [0, %lld)", (long long)n);
+            auto *cnt = (unsigned long long *)c->buf("bb_flag").ensure(8 * (n + 1));
+            GS_HIP(hipMemsetAsync(cnt, 0, 8 * (n + 1), s));
+            k_bb_count<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, E, cnt);
+            uint64_t *nk = (uint64_t *)c->buf("bb_okeys").ensure(8 * (n > E ? n : E));
+            int64_t *ids = (int64_t *)c->buf("bb_order").ensure(8 * (n > E ? n : E));
+            k_bb_relabel_keys<<<grid_for(n, 256, 8192), 256, 0, s>>>(cnt, n, nk, ids);
+            sort_pairs_u64_i64(c, nk, ids, n, 64);
+            int64_t *perm = (int64_t *)b_perm.ensure(8 * n);
+            k_bb_perm<<<grid_for(n, 256, 8192), 256, 0, s>>>(ids, n, perm);
+            int64_t *ms = (int64_t *)b_msrc.ensure(8 * E), *md = (int64_t *)b_mdst.ensure(8 * E);
+            k_bb_map<<<grid_for(E, 256, 8192), 256, 0, s>>>(perm, dsrc, ddst, E, ms, md);
+            GS_HIP(hipGetLastError());
+            osrc = dsrc;
+            odst = ddst;
+            dsrc = ms;
+            ddst = md;
+        }
         const double *dw = (const double *)to_device(c, b_w, w, sizeof(double) * E, loc);
         uint8_t *dkeep = (uint8_t *)out_device(c, b_keep, keep, E ? E : 1, keep_loc);
         unsigned long long *misc = (unsigned long long *)b_misc.ensure(64);
@@ -567,7 +675,8 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
             int *bad = (int *)(misc + 4);
             uint64_t *keys = (uint64_t *)b_keys.ensure(8 * E);
             int64_t *idx = (int64_t *)b_idx.ensure(8 * E);
-            k_bb_keys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, dw, E, n, keys, idx, bad);
+            k_bb_keys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, osrc, odst, dw, E, n, keys, idx,
+                                                             bad);
             int hbad = 0;
             GS_HIP(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
             GS_HIP(hipStreamSynchronize(s));
@@ -666,10 +775,12 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
             if (nsrc > 0) {
                 int64_t *sources = (int64_t *)b_sources.ensure(8 * nsrc);
                 k_bb_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(flag, pos, n, sources);
-                // one 1024-thread workgroup per CU (RMAT-18: 4.1 s; 1,024 x 256 threads 5.2 s,
-                // 512 x 512 4.4 s, 128 x 1,024 5.9 s)
-                int64_t maxslabs = 256;
-                if (const char *e = getenv("GSPARSE_BB_SLABS")) maxslabs = atoi(e) > 0 ? atoi(e) : 256;
+                // large graphs (big search balls): one 1024-thread workgroup per CU (RMAT-18:
+                // 4.1 s; 1,024 x 256 threads 5.2 s, 512 x 512 4.4 s, 128 x 1,024 5.9 s); small
+                // ones (many short searches): 1,024 workgroups of 256 (Roman: 2.2 vs 3.0 ms)
+                const bool big = n > 65536;
+                int64_t maxslabs = big ? 256 : 1024;
+                if (const char *e = getenv("GSPARSE_BB_SLABS")) maxslabs = atoi(e) > 0 ? atoi(e) : maxslabs;
                 int64_t slabs = nsrc < maxslabs ? nsrc : maxslabs;
                 // keep the per-slab working set under ~8 GB
                 int64_t cap = (int64_t)(8e9 / (24.0 * (double)(n ? n : 1)));
@@ -682,7 +793,7 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                 k_bb_fill_u64<<<grid_for(slabs * n, 256, 65536), 256, 0, s>>>(dist, slabs * n,
                                                                                kInfBits);
                 GS_HIP(hipMemsetAsync(qflag, 0, 4 * slabs * n, s));
-                int bt = 1024;
+                int bt = big ? 1024 : 256;
                 if (const char *e = getenv("GSPARSE_BB_THREADS")) bt = atoi(e) == 1024 ? 1024 : atoi(e) == 512 ? 512 : 256;
                 auto kfn = bt == 1024 ? k_bb_sssp<1024> : bt == 512 ? k_bb_sssp<512> : k_bb_sssp<256>;
                 kfn<<<(unsigned)slabs, bt, 0, s>>>(gp, gi, gw, n, sources, nsrc, optr, order,

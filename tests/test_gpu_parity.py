@@ -306,6 +306,21 @@ def test_jaccard_parts_sum_to_whole(gs, nparts):
     assert bits_equal(tot, g["scores_jaccard"])
 
 
+@pytest.mark.parametrize("relabel", ["0", "1"])
+@pytest.mark.parametrize("name", ["karate_test", "directed_dup", "rmat10", "roman2000"])
+def test_backbone_relabel_either_way(gs, name, relabel, monkeypatch):
+    """The degree-ordered node relabeling (automatic for graphs without id locality)
+    forced on and off: the same keep masks as the reference."""
+    monkeypatch.setenv("GSPARSE_BB_RELABEL", relabel)
+    g = load_golden(name)
+    _, data = make(gs, g, with_x=False)
+    for m in ["jaccard", "approx_er"]:
+        if f"backbone_{m}_error" in g:
+            continue
+        _, st = gs.compute_metric_backbone(data, g[f"cost_{m}"], epsilon=1e-9, verbose=False)
+        assert np.array_equal(st["keep_mask"], g[f"backbone_{m}"]), (m, relabel)
+
+
 def test_backbone_rmat12_vs_oracle(gs):
     from gsparse import graphs
 
