@@ -882,7 +882,9 @@ __global__ void __launch_bounds__(256) k_dot_acc(CgGeom G, ChunkArg ch,
                                                  const double *__restrict__ B,
                                                  double *__restrict__ acc) {
     const CgLane ln = cg_lane<CPL>(G);
-    if (!ln.ok) return;
+    // lanes past the block's last column load nothing (their columns may lie
+    // beyond the padded row, and past the buffer on the last row)
+    if (!ln.ok || ln.c >= G.col1) return;
     const int64_t ld = G.ld, c = ln.c;
     const int64_t a = ch.a[ln.t], L = ch.len[ln.t];
     const int64_t n1 = L & ~(int64_t)15, n32 = n1 & ~(int64_t)31;
@@ -1634,7 +1636,9 @@ int gs_er_prepare(gs_ctx *c, int64_t k, double reg, int64_t *m_out) {
         // state
         // row stride padded to 8 doubles: 64-B aligned rows, 16-B vector access
         er.ld = (k + 7) & ~(int64_t)7;
-        size_t nk = sizeof(double) * (size_t)(n ? n : 1) * (size_t)er.ld;
+        // + slack: a 16-B access of a block's last (odd) column reads one column past
+        // the block, which on the last row may be past the row's padding
+        size_t nk = sizeof(double) * ((size_t)(n ? n : 1) * (size_t)er.ld + 256);
         er.X.ensure(nk);
         er.Rr.ensure(nk);
         er.P0.ensure(nk);

@@ -137,7 +137,10 @@ def default_device() -> int:
         return int(env)
     lr = os.environ.get("LOCAL_RANK")
     if lr is not None:
-        return int(lr)
+        # one process per GPU (roman_empire_gpu.py:347); more ranks than visible
+        # GPUs (a rehearsal on a smaller box) share them round-robin
+        cnt = device_count()
+        return int(lr) % cnt if cnt > 0 else int(lr)
     return 0
 
 

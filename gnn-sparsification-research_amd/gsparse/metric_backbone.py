@@ -39,7 +39,9 @@ def backbone_mask(edge_index: np.ndarray, num_nodes: int, edge_weights: np.ndarr
     """Keep mask (bool[E]) of the metric backbone; device computation.
 
     With nparts > 1 only the columns whose source row u has u % nparts == part
-    are decided here (the rest read False): the parts OR to the whole mask."""
+    (u as the library labels it: graphs without id locality are relabeled by
+    degree first) are decided here (the rest read False): the parts OR to the
+    whole mask."""
     ei = np.asarray(edge_index, dtype=np.int64)
     E = ei.shape[1]
     src = np.ascontiguousarray(ei[0])

@@ -119,7 +119,7 @@ def test_approx_er_blas_chunks_vs_oracle(gs, chunked_er, graph, threads, env, mo
     assert bits_equal(er, ref[threads])
 
 
-@pytest.mark.parametrize("mode", ["0", "4"])
+@pytest.mark.parametrize("mode", ["0", "1", "3", "4"])
 def test_er_column_blocks_in_every_mode(gs, chunked_er, mode, monkeypatch):
     """A rank's column block [col0, col1) (the N-GPU split) solved alone, in the
     batched and the resident solver: the blocks' partial sums, added along the
