@@ -278,7 +278,7 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
                     "avg_launch_ms": round(avg_ms, 3), "algorithmic_bytes_per_launch": bytes_per,
                     "launches": p["launches"], "relaxations_per_launch_rank0": relax.value}
         key = f"backbone-{args.bb_graph}" + (str(args.bb_scale) if args.bb_graph == "rmat" else "")
-        traffic, tsrc = pmc_traffic("metric_backbone", key)
+        traffic, tsrc = pmc_traffic("metric_backbone", key) if world == 1 else (None, None)
         if traffic:
             roofline["traffic"] = round(traffic)
             roofline["traffic_source"] = tsrc
@@ -551,7 +551,8 @@ def main():
         avg_ms = p["ms"] / p["launches"]
         bytes_per = p["bytes"] / p["launches"]
         achieved = bytes_per / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = pmc_traffic(name, args.workload)
+        # the committed PMC summaries are of 1-GPU runs (a rank at N > 1 launches a share)
+        traffic, tsrc = pmc_traffic(name, args.workload) if world == 1 else (None, None)
         roofline = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4),
