@@ -337,7 +337,8 @@ def bench_exact_er(args, world, rank, local_rank, dev, dist):
     (dense) scorer the reference runs on small graphs: default Cora-size
     (Chung-Lu stand-in, n=2,708 / 5,278 edges, configs[0]'s graph size), or a
     Roman-like graph of --xer-n nodes.  One step = gs_exact_er end to end
-    (components, grounding, Newton-Schulz on fp64 MFMA, per-edge read-out).
+    (components, grounding, blocked Cholesky + L^-1 on fp64 MFMA -- or
+    Newton-Schulz with GSPARSE_XER_METHOD=ns -- and the per-edge read-out).
     Replicas only: every rank scores its own copy (the dense inverse does not
     shard without an exchange of X every step)."""
     from gsparse import graphs
@@ -396,11 +397,18 @@ def bench_exact_er(args, world, rank, local_rank, dev, dist):
         avg_ms = p["ms"] / p["launches"]
         fl = p["bytes"] / p["launches"]  # executed flops per launch
         achieved = fl / (avg_ms * 1e-3) / 1e12
-        roofline = {"kernel": "k_dgemm<true,64>", "bound": "mfma", "achieved": round(achieved, 2),
+        ns = os.environ.get("GSPARSE_XER_METHOD") == "ns"
+        roofline = {"kernel": "k_dgemm<true,64>" if ns else
+                    "k_chol_diag + k_tile_mm (blocked Cholesky and L^-1, one profiled region)",
+                    "bound": "mfma", "achieved": round(achieved, 2),
                     "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                     "frac": round(achieved / FP64_MFMA_PEAK_TFS, 4), "traffic": None,
                     "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": fl,
-                    "launches": p["launches"], "newton_schulz_steps": eng.exact_er_iterations}
+                    "launches": p["launches"]}
+        if ns:
+            roofline["newton_schulz_steps"] = eng.exact_er_iterations
+        else:
+            roofline["blocks_64"] = eng.exact_er_iterations
         if "exact_er_spmm" in prof:
             q = prof["exact_er_spmm"]
             qa = q["bytes"] / q["ms"] * 1e-6

@@ -17,6 +17,7 @@
 // its upper-triangle tiles run (N^3 flops per step on v_mfma_f64_16x16x4_f64)
 // and X stays exactly symmetric.  ||I - M X||_F is folded into the S kernel.
 #include <cmath>
+#include <cstring>
 
 #include "gs_internal.hpp"
 
@@ -303,6 +304,254 @@ __global__ void k_er_exact_scores(int64_t N, const int32_t *__restrict__ rows,
     }
 }
 
+// ---------------------------------------------------------------- Cholesky path
+// G = M^{-1} from a blocked Cholesky factorisation M = L L^T and W = L^{-1}
+// (64 x 64 blocks; N^3/3 + N^3/3 flops instead of Newton-Schulz's ~N^3 per step
+// over ~log2(cond M) steps), G_uv = (W^T W)_uv = sum_{k >= max(u,v)} W_ku W_kv
+// read from U = W^T.  Per block step k:
+//   k_chol_diag       : A_kk = L_kk L_kk^T in LDS, D_k = L_kk^{-1}
+//   k_tile_mm<PANEL>  : A_ik <- A_ik D_k^T                 (i > k)
+//   k_tile_mm<UPDATE> : A_ij -= A_ik A_jk^T                 (k < j <= i)
+// then, with W = I:
+//   k_tile_mm<INVROW> : W_kj <- D_k W_kj                    (j <= k)
+//   k_tile_mm<INVUPD> : W_ij -= A_ik W_kj                   (i > k, j <= k)
+// Every tile product is 64 x 64 x 64 on v_mfma_f64_16x16x4_f64 (four waves of
+// 2 x 2 MFMA tiles), both operands staged whole in LDS.
+static constexpr int kCb = 64;
+
+__global__ void k_er_dense_rows(int64_t n, int64_t N, const int64_t *__restrict__ ip,
+                                const int32_t *__restrict__ ix, const double *__restrict__ d,
+                                const uint8_t *__restrict__ flag, double *__restrict__ A) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (i >= n || flag[i]) {
+            A[i * N + i] = 1.0;
+            continue;
+        }
+        double deg = 0.0, diag = 0.0;
+        for (int64_t e = ip[i]; e < ip[i + 1]; ++e) {
+            const int32_t k = ix[e];
+            deg += d[e];
+            if (k == i) diag += d[e];
+            else if (!flag[k]) A[i * N + k] = -d[e];
+        }
+        A[i * N + i] = deg - diag;
+    }
+}
+
+__global__ void k_er_identity(int64_t N, double *__restrict__ W) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N;
+         i += (int64_t)gridDim.x * blockDim.x)
+        W[i * N + i] = 1.0;
+}
+
+// factor the diagonal block in LDS; *bad = 1 on a non-positive pivot
+__global__ void __launch_bounds__(256) k_chol_diag(int64_t N, int k, double *__restrict__ A,
+                                                   double *__restrict__ D, int *__restrict__ bad) {
+    __shared__ double S[kCb][kCb + 1];
+    __shared__ double T[kCb][kCb + 1];
+    const int tid = threadIdx.x;
+    double *Akk = A + (int64_t)k * kCb * N + (int64_t)k * kCb;
+    for (int e = tid; e < kCb * kCb; e += 256) {
+        const int r = e / kCb, c = e % kCb;
+        S[r][c] = c <= r ? Akk[(int64_t)r * N + c] : 0.0;
+    }
+    __syncthreads();
+    for (int j = 0; j < kCb; ++j) {
+        if (tid == 0) {
+            const double p = S[j][j];
+            if (!(p > 0.0)) *bad = 1;
+            S[j][j] = sqrt(p > 0.0 ? p : 1.0);
+        }
+        __syncthreads();
+        for (int i = j + 1 + tid; i < kCb; i += 256) S[i][j] = S[i][j] / S[j][j];
+        __syncthreads();
+        const int m = kCb - 1 - j;
+        for (int e = tid; e < m * m; e += 256) {
+            const int i = j + 1 + e / m, l = j + 1 + e % m;
+            if (l <= i) S[i][l] -= S[i][j] * S[l][j];
+        }
+        __syncthreads();
+    }
+    // D = L^{-1}: column c by forward substitution (thread c owns the column)
+    if (tid < kCb) {
+        const int c = tid;
+        for (int i = 0; i < c; ++i) T[i][c] = 0.0;
+        for (int i = c; i < kCb; ++i) {
+            double s = i == c ? 1.0 : 0.0;
+            for (int q = c; q < i; ++q) s -= S[i][q] * T[q][c];
+            T[i][c] = s / S[i][i];
+        }
+    }
+    __syncthreads();
+    double *Dk = D + (int64_t)k * kCb * kCb;
+    for (int e = tid; e < kCb * kCb; e += 256) {
+        const int r = e / kCb, c = e % kCb;
+        Akk[(int64_t)r * N + c] = S[r][c];  // L_kk (zeros above the diagonal)
+        Dk[e] = T[r][c];
+    }
+}
+
+enum { kTilePanel = 0, kTileUpdate = 1, kTileInvRow = 2, kTileInvUpd = 3 };
+
+// row r of the lower triangle (r >= c) holding linear index t of an m x m triangle
+__device__ __forceinline__ void tri_index(int64_t t, int &r, int &c) {
+    int64_t rr = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while (rr * (rr + 1) / 2 > t) --rr;
+    while ((rr + 1) * (rr + 2) / 2 <= t) ++rr;
+    r = (int)rr;
+    c = (int)(t - rr * (rr + 1) / 2);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) k_tile_mm(int64_t N, int nb, int k, double *__restrict__ A,
+                                                 double *__restrict__ W, const double *__restrict__ D) {
+    __shared__ double Xs[kCb][kCb + 1];  // Xs[row][kk]
+    __shared__ double Ys[kCb][kCb + 1];  // Ys[kk][col]
+    typedef double d4 __attribute__((ext_vector_type(4)));
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t t = blockIdx.x;
+    int bi = 0, bj = 0;
+    const double *X;
+    const double *Y;
+    int64_t ldx = N, ldy = N;
+    bool yT = false;
+    double *C;
+    const double *Dk = D + (int64_t)k * kCb * kCb;
+    if (MODE == kTilePanel) {
+        bi = k + 1 + (int)t;
+        bj = k;
+        X = A + (int64_t)bi * kCb * N + (int64_t)k * kCb;
+        Y = Dk;  // Y = D_k^T
+        ldy = kCb;
+        yT = true;
+        C = A + (int64_t)bi * kCb * N + (int64_t)k * kCb;
+    } else if (MODE == kTileUpdate) {
+        int r, c;
+        tri_index(t, r, c);
+        bi = k + 1 + r;
+        bj = k + 1 + c;
+        X = A + (int64_t)bi * kCb * N + (int64_t)k * kCb;
+        Y = A + (int64_t)bj * kCb * N + (int64_t)k * kCb;  // Y = A_jk^T
+        yT = true;
+        C = A + (int64_t)bi * kCb * N + (int64_t)bj * kCb;
+    } else if (MODE == kTileInvRow) {
+        bi = k;
+        bj = (int)t;
+        X = Dk;
+        ldx = kCb;
+        Y = W + (int64_t)k * kCb * N + (int64_t)bj * kCb;
+        C = W + (int64_t)k * kCb * N + (int64_t)bj * kCb;
+    } else {
+        bi = k + 1 + (int)(t / (k + 1));
+        bj = (int)(t % (k + 1));
+        X = A + (int64_t)bi * kCb * N + (int64_t)k * kCb;
+        Y = W + (int64_t)k * kCb * N + (int64_t)bj * kCb;
+        C = W + (int64_t)bi * kCb * N + (int64_t)bj * kCb;
+    }
+    for (int e = tid; e < kCb * kCb; e += 256) {
+        const int r = e / kCb, c = e % kCb;
+        Xs[r][c] = X[(int64_t)r * ldx + c];
+        const double yv = Y[(int64_t)r * ldy + c];
+        if (yT) Ys[c][r] = yv;
+        else Ys[r][c] = yv;
+    }
+    __syncthreads();
+    const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+    d4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < kCb / 4; ++s) {
+        const int kk = s * 4 + (lane >> 4);
+        double a[2], b[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i] = Xs[wr + i * 16 + (lane & 15)][kk];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[j] = Ys[kk][wc + j * 16 + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    // C/D map of the f64 16x16x4 form: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = wr + i * 16 + (lane >> 4) + 4 * r;
+                const int col = wc + j * 16 + (lane & 15);
+                double *cp = C + (int64_t)row * N + col;
+                const double v = acc[i][j][r];
+                if (MODE == kTileUpdate || MODE == kTileInvUpd) *cp = *cp - v;
+                else *cp = v;
+            }
+}
+
+// U = W^T (64 x 64 tiles through LDS)
+__global__ void __launch_bounds__(256) k_er_transpose(int64_t N, const double *__restrict__ W,
+                                                      double *__restrict__ U) {
+    __shared__ double T[kCb][kCb + 1];
+    const int64_t nb = N / kCb;
+    const int64_t bi = blockIdx.x / nb, bj = blockIdx.x % nb;
+    for (int e = threadIdx.x; e < kCb * kCb; e += 256) {
+        const int r = e / kCb, c = e % kCb;
+        T[r][c] = W[(bi * kCb + r) * N + bj * kCb + c];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < kCb * kCb; e += 256) {
+        const int r = e / kCb, c = e % kCb;
+        U[(bj * kCb + r) * N + bi * kCb + c] = T[c][r];
+    }
+}
+
+// g[u] = G_uu = sum_{k >= u} U_uk^2, one wave per row
+__global__ void __launch_bounds__(256) k_er_gdiag(int64_t n, int64_t N, const double *__restrict__ U,
+                                                  double *__restrict__ g) {
+    const int64_t u = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (u >= n) return;
+    double s = 0.0;
+    for (int64_t k = u + lane; k < N; k += 64) {
+        const double x = U[u * N + k];
+        s += x * x;
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if (lane == 0) g[u] = s;
+}
+
+// r_eff in CSR order, one wave per entry: G_uv = sum_{k >= max(u,v)} U_uk U_vk
+__global__ void __launch_bounds__(256) k_er_chol_scores(int64_t N, const int32_t *__restrict__ rows,
+                                                        const int32_t *__restrict__ ix, int64_t nnz,
+                                                        const uint8_t *__restrict__ flag,
+                                                        const double *__restrict__ U,
+                                                        const double *__restrict__ g,
+                                                        double *__restrict__ out) {
+    const int64_t e = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (e >= nnz) return;
+    const int64_t u = rows[e], v = ix[e];
+    const bool fu = flag[u], fv = flag[v];
+    double s = 0.0;
+    if (!fu && !fv) {
+        const int64_t k0 = u > v ? u : v;
+        for (int64_t k = k0 + lane; k < N; k += 64) s += U[u * N + k] * U[v * N + k];
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if (lane == 0) {
+        const double guu = fu ? 0.0 : g[u];
+        const double gvv = fv ? 0.0 : g[v];
+        const double guv = (fu || fv) ? 0.0 : s;
+        const double r = (guu + gvv) - 2.0 * guv;
+        out[e] = r > 1e-10 ? r : 1e-10;
+    }
+}
+
 }  // namespace gs
 
 using namespace gs;
@@ -359,6 +608,53 @@ extern "C" int gs_exact_er(gs_ctx *c, double *out, int loc, int32_t *iterations)
             k_er_ground_mark<<<grid_for(N, 256, 8192), 256, 0, st>>>(n, N, lab, best, flag);
             k_er_rownorm<<<grid_for(n, 256, 2048), 256, 0, st>>>(n, ip, ix, dd, flag, mx);
             const size_t mb = sizeof(double) * (size_t)N * (size_t)N;
+            const char *meth = getenv("GSPARSE_XER_METHOD");
+            if (!meth || strcmp(meth, "ns") != 0) {
+                // blocked Cholesky + triangular inverse (see k_chol_diag)
+                const int nb = (int)(N / kCb);
+                double *A = (double *)c->buf("xer_X").ensure(mb);
+                double *W = (double *)c->buf("xer_S").ensure(mb);
+                double *D = (double *)c->buf("xer_D").ensure(sizeof(double) * (size_t)nb * kCb * kCb);
+                double *gd = (double *)c->buf("xer_g").ensure(sizeof(double) * (size_t)n);
+                GS_HIP(hipMemsetAsync(flags, 0, 4, st));
+                GS_HIP(hipMemsetAsync(A, 0, mb, st));
+                k_er_dense_rows<<<grid_for(N, 256, 8192), 256, 0, st>>>(n, N, ip, ix, dd, flag, A);
+                double fl_upd = 0.0;
+                hipEvent_t t0 = prof_begin(c);
+                for (int k = 0; k < nb; ++k) {
+                    k_chol_diag<<<1, 256, 0, st>>>(N, k, A, D, flags);
+                    const int m = nb - 1 - k;
+                    if (m > 0) {
+                        k_tile_mm<kTilePanel><<<(unsigned)m, 256, 0, st>>>(N, nb, k, A, W, D);
+                        k_tile_mm<kTileUpdate><<<(unsigned)((int64_t)m * (m + 1) / 2), 256, 0, st>>>(
+                            N, nb, k, A, W, D);
+                        fl_upd += 2.0 * kCb * kCb * kCb * ((double)m * (m + 1) / 2 + m);
+                    }
+                }
+                GS_HIP(hipMemsetAsync(W, 0, mb, st));
+                k_er_identity<<<grid_for(N, 256, 8192), 256, 0, st>>>(N, W);
+                for (int k = 0; k < nb; ++k) {
+                    k_tile_mm<kTileInvRow><<<(unsigned)(k + 1), 256, 0, st>>>(N, nb, k, A, W, D);
+                    const int m = nb - 1 - k;
+                    if (m > 0)
+                        k_tile_mm<kTileInvUpd><<<(unsigned)((int64_t)m * (k + 1)), 256, 0, st>>>(
+                            N, nb, k, A, W, D);
+                    fl_upd += 2.0 * kCb * kCb * kCb * ((double)m * (k + 1) + (k + 1));
+                }
+                // the factorisation + inverse as one profiled region (flops executed on MFMA)
+                prof_end(c, t0, "exact_er_dgemm", fl_upd);
+                int bad = 0;
+                GS_HIP(hipMemcpyAsync(&bad, flags, 4, hipMemcpyDeviceToHost, st));
+                GS_HIP(hipStreamSynchronize(st));
+                GS_CHECK(!bad, GS_EHIP, "Cholesky: non-positive pivot (M not positive definite)");
+                k_er_transpose<<<(unsigned)((int64_t)nb * nb), 256, 0, st>>>(N, W, A);
+                k_er_gdiag<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(n, N, A, gd);
+                if (nnz)
+                    k_er_chol_scores<<<(unsigned)((nnz + 3) / 4), 256, 0, st>>>(
+                        N, g.rows.as<int32_t>(), ix, nnz, flag, A, gd, dout);
+                GS_HIP(hipGetLastError());
+                it_done = nb;
+            } else {
             double *X = (double *)c->buf("xer_X").ensure(mb);
             double *X2 = (double *)c->buf("xer_X2").ensure(mb);
             double *S = (double *)c->buf("xer_S").ensure(mb);
@@ -411,6 +707,7 @@ extern "C" int gs_exact_er(gs_ctx *c, double *out, int loc, int32_t *iterations)
                 k_er_exact_scores<<<grid_for(nnz, 256, 8192), 256, 0, st>>>(
                     N, g.rows.as<int32_t>(), ix, nnz, flag, X, dout);
             GS_HIP(hipGetLastError());
+            }
         }
         finish_out(c, out, dout, sizeof(double) * nnz, loc);
         if (iterations) *iterations = it_done;
