@@ -493,6 +493,93 @@ __global__ void __launch_bounds__(256) k_tile_mm(int64_t N, int nb, int k, doubl
             }
 }
 
+// Rank-(64 kb) tile updates, C -= sum_{q < kb} X_q Y_q over a tile region:
+//   CHOL: C = A_ij, X_q = A_{i,k0+q}, Y_q = A_{j,k0+q}^T   (trailing lower triangle)
+//   INV : C = W_ij, X_q = A_{i,k0+q}, Y_q = W_{k0+q,j}
+// tri: tiles (i, j) with lo <= j <= i < hi; else i in [ilo, ihi), j in [jlo, jhi).
+// Wider K (kb = 4: 256) reads and rewrites each C tile once per 4 block steps.
+struct TileJob {
+    int k0, kb;
+    int ilo, ihi, jlo, jhi;
+    int tri;
+};
+
+template <bool INV>
+__global__ void __launch_bounds__(256) k_tile_upd(int64_t N, TileJob J, double *__restrict__ A,
+                                                  double *__restrict__ W) {
+    __shared__ double Xs[kCb][kCb + 1];
+    __shared__ double Ys[kCb][kCb + 1];
+    typedef double d4 __attribute__((ext_vector_type(4)));
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t t = blockIdx.x;
+    int bi, bj;
+    if (J.tri) {
+        int r, c;
+        tri_index(t, r, c);
+        bi = J.ilo + r;
+        bj = J.ilo + c;
+    } else {
+        const int w = J.jhi - J.jlo;
+        bi = J.ilo + (int)(t / w);
+        bj = J.jlo + (int)(t % w);
+    }
+    double *C = (INV ? W : A) + (int64_t)bi * kCb * N + (int64_t)bj * kCb;
+    const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+    d4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int q = 0; q < J.kb; ++q) {
+        const int kq = J.k0 + q;
+        const double *X = A + (int64_t)bi * kCb * N + (int64_t)kq * kCb;
+        const double *Y = INV ? W + (int64_t)kq * kCb * N + (int64_t)bj * kCb
+                              : A + (int64_t)bj * kCb * N + (int64_t)kq * kCb;
+        for (int e = tid; e < kCb * kCb; e += 256) {
+            const int r = e / kCb, c = e % kCb;
+            Xs[r][c] = X[(int64_t)r * N + c];
+            const double yv = Y[(int64_t)r * N + c];
+            if (INV) Ys[r][c] = yv;
+            else Ys[c][r] = yv;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < kCb / 4; ++s) {
+            const int kk = s * 4 + (lane >> 4);
+            double a[2], b[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) a[i] = Xs[wr + i * 16 + (lane & 15)][kk];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b[j] = Ys[kk][wc + j * 16 + (lane & 15)];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = wr + i * 16 + (lane >> 4) + 4 * r;
+                const int col = wc + j * 16 + (lane & 15);
+                double *cp = C + (int64_t)row * N + col;
+                *cp = *cp - acc[i][j][r];
+            }
+}
+
+static unsigned tile_count(const TileJob &J) {
+    if (J.tri) {
+        const int64_t m = J.ihi - J.ilo;
+        return (unsigned)(m * (m + 1) / 2);
+    }
+    return (unsigned)((int64_t)(J.ihi - J.ilo) * (J.jhi - J.jlo));
+}
+
 // U = W^T (64 x 64 tiles through LDS)
 __global__ void __launch_bounds__(256) k_er_transpose(int64_t N, const double *__restrict__ W,
                                                       double *__restrict__ U) {
@@ -620,26 +707,47 @@ extern "C" int gs_exact_er(gs_ctx *c, double *out, int loc, int32_t *iterations)
                 GS_HIP(hipMemsetAsync(A, 0, mb, st));
                 k_er_dense_rows<<<grid_for(N, 256, 8192), 256, 0, st>>>(n, N, ip, ix, dd, flag, A);
                 double fl_upd = 0.0;
+                const double tf = 2.0 * kCb * kCb * kCb;  // flops of one 64^3 tile product
+                // block columns per panel: the trailing update runs at K = 64 P and rewrites
+                // each C tile once per P block steps (Roman-like n = 22,662: P = 1 0.59 s,
+                // 2 0.47 s, 4 0.39 s, 8 0.37 s)
+                int P = 8;
+                if (const char *e = getenv("GSPARSE_XER_PANEL")) P = atoi(e) >= 1 && atoi(e) <= 16 ? atoi(e) : 8;
+                auto upd = [&](bool inv, const TileJob &J) {
+                    const unsigned cnt = tile_count(J);
+                    if (!cnt || J.kb <= 0) return;
+                    if (inv) k_tile_upd<true><<<cnt, 256, 0, st>>>(N, J, A, W);
+                    else k_tile_upd<false><<<cnt, 256, 0, st>>>(N, J, A, W);
+                    fl_upd += tf * J.kb * (double)cnt;
+                };
                 hipEvent_t t0 = prof_begin(c);
-                for (int k = 0; k < nb; ++k) {
-                    k_chol_diag<<<1, 256, 0, st>>>(N, k, A, D, flags);
-                    const int m = nb - 1 - k;
-                    if (m > 0) {
-                        k_tile_mm<kTilePanel><<<(unsigned)m, 256, 0, st>>>(N, nb, k, A, W, D);
-                        k_tile_mm<kTileUpdate><<<(unsigned)((int64_t)m * (m + 1) / 2), 256, 0, st>>>(
-                            N, nb, k, A, W, D);
-                        fl_upd += 2.0 * kCb * kCb * kCb * ((double)m * (m + 1) / 2 + m);
+                for (int k0 = 0; k0 < nb; k0 += P) {
+                    const int kend = k0 + P < nb ? k0 + P : nb;
+                    for (int k = k0; k < kend; ++k) {
+                        k_chol_diag<<<1, 256, 0, st>>>(N, k, A, D, flags);
+                        const int m = nb - 1 - k;
+                        if (m > 0) {
+                            k_tile_mm<kTilePanel><<<(unsigned)m, 256, 0, st>>>(N, nb, k, A, W, D);
+                            fl_upd += tf * m;
+                        }
+                        // the panel's own later columns (i >= j, k < j < kend), one K = 64 step
+                        for (int j = k + 1; j < kend; ++j) upd(false, TileJob{k, 1, j, nb, j, j + 1, 0});
                     }
+                    // the trailing lower triangle, K = 64 (kend - k0)
+                    upd(false, TileJob{k0, kend - k0, kend, nb, kend, nb, 1});
                 }
                 GS_HIP(hipMemsetAsync(W, 0, mb, st));
                 k_er_identity<<<grid_for(N, 256, 8192), 256, 0, st>>>(N, W);
-                for (int k = 0; k < nb; ++k) {
-                    k_tile_mm<kTileInvRow><<<(unsigned)(k + 1), 256, 0, st>>>(N, nb, k, A, W, D);
-                    const int m = nb - 1 - k;
-                    if (m > 0)
-                        k_tile_mm<kTileInvUpd><<<(unsigned)((int64_t)m * (k + 1)), 256, 0, st>>>(
-                            N, nb, k, A, W, D);
-                    fl_upd += 2.0 * kCb * kCb * kCb * ((double)m * (k + 1) + (k + 1));
+                for (int k0 = 0; k0 < nb; k0 += P) {
+                    const int kend = k0 + P < nb ? k0 + P : nb;
+                    for (int k = k0; k < kend; ++k) {
+                        k_tile_mm<kTileInvRow><<<(unsigned)(k + 1), 256, 0, st>>>(N, nb, k, A, W, D);
+                        fl_upd += tf * (k + 1);
+                        // rows of the panel below k (W_ij -= L_ik W_kj, j <= k)
+                        upd(true, TileJob{k, 1, k + 1, kend, 0, k + 1, 0});
+                    }
+                    // rows below the panel: W_ij -= sum_{k in panel} L_ik W_kj, j < kend
+                    upd(true, TileJob{k0, kend - k0, kend, nb, 0, kend, 0});
                 }
                 // the factorisation + inverse as one profiled region (flops executed on MFMA)
                 prof_end(c, t0, "exact_er_dgemm", fl_upd);
