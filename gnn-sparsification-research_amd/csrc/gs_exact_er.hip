@@ -345,16 +345,21 @@ __global__ void k_er_identity(int64_t N, double *__restrict__ W) {
         W[i * N + i] = 1.0;
 }
 
-// factor the diagonal block in LDS; *bad = 1 on a non-positive pivot
+// factor the diagonal block in LDS (right-looking, all 256 threads); *bad = 1 on
+// a non-positive pivot.  D = L^{-1} by 2 x 2 blocks of 32:
+// T11 = L11^{-1}, T22 = L22^{-1} (one thread per column, both halves at once),
+// then T21 = -T22 (L21 T11) on all 256 threads.
 __global__ void __launch_bounds__(256) k_chol_diag(int64_t N, int k, double *__restrict__ A,
                                                    double *__restrict__ D, int *__restrict__ bad) {
     __shared__ double S[kCb][kCb + 1];
     __shared__ double T[kCb][kCb + 1];
+    __shared__ double Z[32][33];
     const int tid = threadIdx.x;
     double *Akk = A + (int64_t)k * kCb * N + (int64_t)k * kCb;
     for (int e = tid; e < kCb * kCb; e += 256) {
         const int r = e / kCb, c = e % kCb;
         S[r][c] = c <= r ? Akk[(int64_t)r * N + c] : 0.0;
+        T[r][c] = 0.0;
     }
     __syncthreads();
     for (int j = 0; j < kCb; ++j) {
@@ -373,15 +378,30 @@ __global__ void __launch_bounds__(256) k_chol_diag(int64_t N, int k, double *__r
         }
         __syncthreads();
     }
-    // D = L^{-1}: column c by forward substitution (thread c owns the column)
-    if (tid < kCb) {
-        const int c = tid;
-        for (int i = 0; i < c; ++i) T[i][c] = 0.0;
-        for (int i = c; i < kCb; ++i) {
+    // diagonal halves: thread c < 32 -> column c of T11, 32 <= c < 64 -> column of T22
+    if (tid < 64) {
+        const int c = tid, lo = c < 32 ? 0 : 32, hi = lo + 32;
+        for (int i = c; i < hi; ++i) {
             double s = i == c ? 1.0 : 0.0;
             for (int q = c; q < i; ++q) s -= S[i][q] * T[q][c];
             T[i][c] = s / S[i][i];
         }
+        (void)lo;
+    }
+    __syncthreads();
+    // Z = L21 T11 (32 x 32), then T21 = -T22 Z
+    for (int e = tid; e < 32 * 32; e += 256) {
+        const int r = e / 32, c = e % 32;
+        double s = 0.0;
+        for (int q = c; q < 32; ++q) s += S[32 + r][q] * T[q][c];
+        Z[r][c] = s;
+    }
+    __syncthreads();
+    for (int e = tid; e < 32 * 32; e += 256) {
+        const int r = e / 32, c = e % 32;
+        double s = 0.0;
+        for (int q = 0; q <= r; ++q) s += T[32 + r][32 + q] * Z[q][c];
+        T[32 + r][c] = -s;
     }
     __syncthreads();
     double *Dk = D + (int64_t)k * kCb * kCb;
