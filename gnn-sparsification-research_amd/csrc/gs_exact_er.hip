@@ -659,6 +659,106 @@ __global__ void __launch_bounds__(256) k_er_chol_scores(int64_t N, const int32_t
     }
 }
 
+// Connected components of the resident graph: label = smallest node id of the
+// component (min-label propagation with pointer jumping); device buffer.
+int32_t *components(gs_ctx *c) {
+    Graph &g = c->g;
+    hipStream_t st = c->stream;
+    const int64_t n = g.n, nnz = g.nnz;
+    auto *flags = (int *)c->buf("cc_flags").ensure(64);
+    auto *lab = (int32_t *)c->buf("xer_lab").ensure(4 * (n ? n : 1));
+    if (!n) return lab;
+    k_cc_init<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, lab);
+    for (int round = 0; round < 4096; ++round) {
+        GS_HIP(hipMemsetAsync(flags, 0, 4, st));
+        if (nnz)
+            k_cc_hook<<<grid_for(nnz, 256, 8192), 256, 0, st>>>(g.rows.as<int32_t>(),
+                                                                g.indices.as<int32_t>(), nnz, lab,
+                                                                flags);
+        k_cc_jump<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, lab);
+        int ch = 0;
+        GS_HIP(hipMemcpyAsync(&ch, flags, 4, hipMemcpyDeviceToHost, st));
+        GS_HIP(hipStreamSynchronize(st));
+        if (!ch) break;
+    }
+    return lab;
+}
+
+// U = W^T for an N x N matrix (N a multiple of 64)
+void transpose_square(gs_ctx *c, int64_t N, const double *W, double *U) {
+    const int64_t nb = N / kCb;
+    k_er_transpose<<<(unsigned)(nb * nb), 256, 0, c->stream>>>(N, W, U);
+    GS_HIP(hipGetLastError());
+}
+
+// W = L^{-1} for the grounded M of the resident graph (identity rows where
+// flag is set), M = L L^T by the blocked Cholesky of k_chol_diag / k_tile_mm /
+// k_tile_upd; A and W are N x N scratch (A ends holding L).
+void grounded_inverse(gs_ctx *c, int64_t N, const uint8_t *flag, double *A, double *W) {
+    Graph &g = c->g;
+    hipStream_t st = c->stream;
+    const int64_t n = g.n;
+    const size_t mb = sizeof(double) * (size_t)N * (size_t)N;
+    const int64_t *ip = g.indptr.as<int64_t>();
+    const int32_t *ix = g.indices.as<int32_t>();
+    const double *dd = g.data.as<double>();
+    auto *flags = (int *)c->buf("chol_flags").ensure(64);
+    const int nb = (int)(N / kCb);
+    double *D = (double *)c->buf("xer_D").ensure(sizeof(double) * (size_t)nb * kCb * kCb);
+    GS_HIP(hipMemsetAsync(flags, 0, 4, st));
+    GS_HIP(hipMemsetAsync(A, 0, mb, st));
+    k_er_dense_rows<<<grid_for(N, 256, 8192), 256, 0, st>>>(n, N, ip, ix, dd, flag, A);
+    double fl_upd = 0.0;
+    const double tf = 2.0 * kCb * kCb * kCb;  // flops of one 64^3 tile product
+    // block columns per panel: the trailing update runs at K = 64 P and rewrites
+    // each C tile once per P block steps (Roman-like n = 22,662: P = 1 0.59 s,
+    // 2 0.47 s, 4 0.39 s, 8 0.37 s)
+    int P = 8;
+    if (const char *e = getenv("GSPARSE_XER_PANEL")) P = atoi(e) >= 1 && atoi(e) <= 16 ? atoi(e) : 8;
+    auto upd = [&](bool inv, const TileJob &J) {
+        const unsigned cnt = tile_count(J);
+        if (!cnt || J.kb <= 0) return;
+        if (inv) k_tile_upd<true><<<cnt, 256, 0, st>>>(N, J, A, W);
+        else k_tile_upd<false><<<cnt, 256, 0, st>>>(N, J, A, W);
+        fl_upd += tf * J.kb * (double)cnt;
+    };
+    hipEvent_t t0 = prof_begin(c);
+    for (int k0 = 0; k0 < nb; k0 += P) {
+        const int kend = k0 + P < nb ? k0 + P : nb;
+        for (int k = k0; k < kend; ++k) {
+            k_chol_diag<<<1, 256, 0, st>>>(N, k, A, D, flags);
+            const int m = nb - 1 - k;
+            if (m > 0) {
+                k_tile_mm<kTilePanel><<<(unsigned)m, 256, 0, st>>>(N, nb, k, A, W, D);
+                fl_upd += tf * m;
+            }
+            // the panel's own later columns (i >= j, k < j < kend), one K = 64 step
+            for (int j = k + 1; j < kend; ++j) upd(false, TileJob{k, 1, j, nb, j, j + 1, 0});
+        }
+        // the trailing lower triangle, K = 64 (kend - k0)
+        upd(false, TileJob{k0, kend - k0, kend, nb, kend, nb, 1});
+    }
+    GS_HIP(hipMemsetAsync(W, 0, mb, st));
+    k_er_identity<<<grid_for(N, 256, 8192), 256, 0, st>>>(N, W);
+    for (int k0 = 0; k0 < nb; k0 += P) {
+        const int kend = k0 + P < nb ? k0 + P : nb;
+        for (int k = k0; k < kend; ++k) {
+            k_tile_mm<kTileInvRow><<<(unsigned)(k + 1), 256, 0, st>>>(N, nb, k, A, W, D);
+            fl_upd += tf * (k + 1);
+            // rows of the panel below k (W_ij -= L_ik W_kj, j <= k)
+            upd(true, TileJob{k, 1, k + 1, kend, 0, k + 1, 0});
+        }
+        // rows below the panel: W_ij -= sum_{k in panel} L_ik W_kj, j < kend
+        upd(true, TileJob{k0, kend - k0, kend, nb, 0, kend, 0});
+    }
+    // the factorisation + inverse as one profiled region (flops executed on MFMA)
+    prof_end(c, t0, "exact_er_dgemm", fl_upd);
+    int bad = 0;
+    GS_HIP(hipMemcpyAsync(&bad, flags, 4, hipMemcpyDeviceToHost, st));
+    GS_HIP(hipStreamSynchronize(st));
+    GS_CHECK(!bad, GS_EHIP, "Cholesky: non-positive pivot (M not positive definite)");
+}
+
 }  // namespace gs
 
 using namespace gs;
@@ -690,19 +790,7 @@ extern "C" int gs_exact_er(gs_ctx *c, double *out, int loc, int32_t *iterations)
                 GS_CHECK(!asym, GS_EUNSUPPORTED,
                          "exact effective resistance needs symmetric edge weights");
             }
-            auto *lab = (int32_t *)c->buf("xer_lab").ensure(4 * n);
-            k_cc_init<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, lab);
-            for (int round = 0; round < 4096; ++round) {
-                GS_HIP(hipMemsetAsync(flags, 0, 4, st));
-                if (nnz)
-                    k_cc_hook<<<grid_for(nnz, 256, 8192), 256, 0, st>>>(
-                        g.rows.as<int32_t>(), g.indices.as<int32_t>(), nnz, lab, flags);
-                k_cc_jump<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, lab);
-                int ch = 0;
-                GS_HIP(hipMemcpyAsync(&ch, flags, 4, hipMemcpyDeviceToHost, st));
-                GS_HIP(hipStreamSynchronize(st));
-                if (!ch) break;
-            }
+            int32_t *lab = components(c);
             const int64_t *ip = g.indptr.as<int64_t>();
             const int32_t *ix = g.indices.as<int32_t>();
             const double *dd = g.data.as<double>();
@@ -721,60 +809,8 @@ extern "C" int gs_exact_er(gs_ctx *c, double *out, int loc, int32_t *iterations)
                 const int nb = (int)(N / kCb);
                 double *A = (double *)c->buf("xer_X").ensure(mb);
                 double *W = (double *)c->buf("xer_S").ensure(mb);
-                double *D = (double *)c->buf("xer_D").ensure(sizeof(double) * (size_t)nb * kCb * kCb);
                 double *gd = (double *)c->buf("xer_g").ensure(sizeof(double) * (size_t)n);
-                GS_HIP(hipMemsetAsync(flags, 0, 4, st));
-                GS_HIP(hipMemsetAsync(A, 0, mb, st));
-                k_er_dense_rows<<<grid_for(N, 256, 8192), 256, 0, st>>>(n, N, ip, ix, dd, flag, A);
-                double fl_upd = 0.0;
-                const double tf = 2.0 * kCb * kCb * kCb;  // flops of one 64^3 tile product
-                // block columns per panel: the trailing update runs at K = 64 P and rewrites
-                // each C tile once per P block steps (Roman-like n = 22,662: P = 1 0.59 s,
-                // 2 0.47 s, 4 0.39 s, 8 0.37 s)
-                int P = 8;
-                if (const char *e = getenv("GSPARSE_XER_PANEL")) P = atoi(e) >= 1 && atoi(e) <= 16 ? atoi(e) : 8;
-                auto upd = [&](bool inv, const TileJob &J) {
-                    const unsigned cnt = tile_count(J);
-                    if (!cnt || J.kb <= 0) return;
-                    if (inv) k_tile_upd<true><<<cnt, 256, 0, st>>>(N, J, A, W);
-                    else k_tile_upd<false><<<cnt, 256, 0, st>>>(N, J, A, W);
-                    fl_upd += tf * J.kb * (double)cnt;
-                };
-                hipEvent_t t0 = prof_begin(c);
-                for (int k0 = 0; k0 < nb; k0 += P) {
-                    const int kend = k0 + P < nb ? k0 + P : nb;
-                    for (int k = k0; k < kend; ++k) {
-                        k_chol_diag<<<1, 256, 0, st>>>(N, k, A, D, flags);
-                        const int m = nb - 1 - k;
-                        if (m > 0) {
-                            k_tile_mm<kTilePanel><<<(unsigned)m, 256, 0, st>>>(N, nb, k, A, W, D);
-                            fl_upd += tf * m;
-                        }
-                        // the panel's own later columns (i >= j, k < j < kend), one K = 64 step
-                        for (int j = k + 1; j < kend; ++j) upd(false, TileJob{k, 1, j, nb, j, j + 1, 0});
-                    }
-                    // the trailing lower triangle, K = 64 (kend - k0)
-                    upd(false, TileJob{k0, kend - k0, kend, nb, kend, nb, 1});
-                }
-                GS_HIP(hipMemsetAsync(W, 0, mb, st));
-                k_er_identity<<<grid_for(N, 256, 8192), 256, 0, st>>>(N, W);
-                for (int k0 = 0; k0 < nb; k0 += P) {
-                    const int kend = k0 + P < nb ? k0 + P : nb;
-                    for (int k = k0; k < kend; ++k) {
-                        k_tile_mm<kTileInvRow><<<(unsigned)(k + 1), 256, 0, st>>>(N, nb, k, A, W, D);
-                        fl_upd += tf * (k + 1);
-                        // rows of the panel below k (W_ij -= L_ik W_kj, j <= k)
-                        upd(true, TileJob{k, 1, k + 1, kend, 0, k + 1, 0});
-                    }
-                    // rows below the panel: W_ij -= sum_{k in panel} L_ik W_kj, j < kend
-                    upd(true, TileJob{k0, kend - k0, kend, nb, 0, kend, 0});
-                }
-                // the factorisation + inverse as one profiled region (flops executed on MFMA)
-                prof_end(c, t0, "exact_er_dgemm", fl_upd);
-                int bad = 0;
-                GS_HIP(hipMemcpyAsync(&bad, flags, 4, hipMemcpyDeviceToHost, st));
-                GS_HIP(hipStreamSynchronize(st));
-                GS_CHECK(!bad, GS_EHIP, "Cholesky: non-positive pivot (M not positive definite)");
+                grounded_inverse(c, N, flag, A, W);
                 k_er_transpose<<<(unsigned)((int64_t)nb * nb), 256, 0, st>>>(N, W, A);
                 k_er_gdiag<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(n, N, A, gd);
                 if (nnz)

@@ -172,6 +172,14 @@ void sort_pairs_u64_i64(gs_ctx *c, uint64_t *keys, int64_t *vals, int64_t n, int
 void ensure_transpose(gs_ctx *c);
 
 // Whole-graph Jaccard of a symmetric graph (gs_jaccard.hip)
-void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts);
+// counts != 0: |N(u) ∩ N(v)| per entry instead of the Jaccard ratio
+void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts = 0);
+
+// Dense grounded-Laplacian machinery (gs_exact_er.hip): component labels of the
+// resident graph (smallest node id per component, device), and W = L^{-1} of
+// M = L L^T for the grounded M (identity rows where flag[u], N x N scratch A, W)
+int32_t *components(gs_ctx *c);
+void grounded_inverse(gs_ctx *c, int64_t N, const uint8_t *flag, double *A, double *W);
+void transpose_square(gs_ctx *c, int64_t N, const double *W, double *U);
 
 }  // namespace gs

@@ -42,6 +42,11 @@ __device__ __forceinline__ double jac_value(int64_t inter, int64_t du, int64_t d
     return uni > 0.0 ? (double)inter / uni : 0.0;
 }
 
+// counts != 0: the raw |N(u) ∩ N(v)| (gs_common_neighbors) instead of the ratio
+__device__ __forceinline__ double jac_out(int counts, int64_t inter, int64_t du, int64_t dv) {
+    return counts ? (double)inter : jac_value(inter, du, dv);
+}
+
 __host__ __device__ __forceinline__ int jac_class(int64_t d) {
     if (d <= kJacLight) return -1;
     if (d <= 1024) return 0;
@@ -145,7 +150,8 @@ __global__ void __launch_bounds__(256) k_jac_light(const int64_t *__restrict__ i
                                                    const int32_t *__restrict__ ix,
                                                    const int32_t *__restrict__ rows,
                                                    const int64_t *__restrict__ rev, int64_t e0,
-                                                   int64_t e1, double *__restrict__ out) {
+                                                   int64_t e1, double *__restrict__ out,
+                                                   int counts) {
     for (int64_t e = e0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < e1;
          e += (int64_t)gridDim.x * blockDim.x) {
         const int32_t u = rows[e];
@@ -161,7 +167,7 @@ __global__ void __launch_bounds__(256) k_jac_light(const int64_t *__restrict__ i
             i += (x <= y);
             j += (y <= x);
         }
-        const double val = jac_value(cnt, du, dv);
+        const double val = jac_out(counts, cnt, du, dv);
         out[e] = val;
         out[rev[e]] = val;
     }
@@ -233,7 +239,8 @@ template <class Probe>
 __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
                                                  const int64_t *__restrict__ rev, int64_t du,
                                                  int64_t lo, const JacStage &st,
-                                                 double *__restrict__ out, const Probe &pr) {
+                                                 double *__restrict__ out, const Probe &pr,
+                                                 int counts) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     for (int k = wave; k < st.nbig; k += nw) {
         const int64_t b = st.b[k], dv = st.dv[k];
@@ -256,7 +263,7 @@ __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
         }
         if (lane == 0) {
             const int64_t e = lo + st.off[k];
-            const double val = jac_value(cnt, du, dv);
+            const double val = jac_out(counts, cnt, du, dv);
             out[e] = val;
             out[rev[e]] = val;
         }
@@ -274,7 +281,7 @@ __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
         const int64_t cnt = __popcll(__ballot(hit) & gmask);
         if (ok && gl == 0) {
             const int64_t e = lo + st.off[k];
-            const double val = jac_value(cnt, du, dv);
+            const double val = jac_out(counts, cnt, du, dv);
             out[e] = val;
             out[rev[e]] = val;
         }
@@ -300,7 +307,7 @@ __global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ i
                                                    const int32_t *__restrict__ ntask,
                                                    const int32_t *__restrict__ trow,
                                                    const int32_t *__restrict__ ti, int64_t t0,
-                                                   double *__restrict__ out) {
+                                                   double *__restrict__ out, int counts) {
     // 4-slot buckets (one 16-B LDS read per probe step); a bucket fills from
     // slot 0 up, so a bucket with a free slot 3 ends an unsuccessful search
     __shared__ int4 tab[C / 4];
@@ -330,7 +337,7 @@ __global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ i
         }
     }
     __syncthreads();
-    jac_probe_staged(ix, rev, du, lo, st, out, JacHashProbe{tab, shift, mask});
+    jac_probe_staged(ix, rev, du, lo, st, out, JacHashProbe{tab, shift, mask}, counts);
 }
 
 __global__ void k_jac_bitmap_build(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
@@ -354,7 +361,7 @@ __global__ void __launch_bounds__(1024) k_jac_bitmap(const int64_t *__restrict__
                                                      const int32_t *__restrict__ tslot,
                                                      int64_t t0, int32_t g0, int64_t words,
                                                      const uint32_t *__restrict__ bm,
-                                                     double *__restrict__ out) {
+                                                     double *__restrict__ out, int counts) {
     const int64_t t = t0 + blockIdx.x;
     const int32_t u = trow[t];
     int64_t a, du, lo, hi;
@@ -365,7 +372,7 @@ __global__ void __launch_bounds__(1024) k_jac_bitmap(const int64_t *__restrict__
     __syncthreads();
     jac_stage(ip, ix, u, du, lo, hi, st);
     __syncthreads();
-    jac_probe_staged(ix, rev, du, lo, st, out, JacBitProbe{m});
+    jac_probe_staged(ix, rev, du, lo, st, out, JacBitProbe{m}, counts);
 }
 
 // B_J for a symmetric graph: 8 * sum_u d_u^2 + 12 * nnz
@@ -385,7 +392,7 @@ __global__ void k_jac_bytes(const int64_t *__restrict__ ip, int64_t n,
 // `part` of `nparts` of it: that part's share of the light entries and of
 // every class's task list (both CSR entries of each pair written), every
 // other entry 0.0 -- the nparts outputs sum to the whole.
-void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts) {
+void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts) {
     Graph &g = c->g;
     const int64_t n = g.n, nnz = g.nnz;
     if (!nnz) return;
@@ -419,7 +426,7 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts) {
         const int64_t e0 = share(nnz, part), e1 = share(nnz, part + 1);
         if (e1 > e0)
             k_jac_light<<<grid_for(e1 - e0, 256, 65536), 256, 0, st>>>(
-                ip, ix, g.rows.as<int32_t>(), rev, e0, e1, out);
+                ip, ix, g.rows.as<int32_t>(), rev, e0, e1, out, counts);
     }
     GS_HIP(hipGetLastError());
     unsigned long long htot[kJacClasses + 1];
@@ -452,13 +459,13 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts) {
         const unsigned nb = (unsigned)(thi - tlo);
         if (k < kJacBitmap && !nb) continue;
         if (k == 0) {
-            k_jac_hash<2048><<<nb, 256, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out);
+            k_jac_hash<2048><<<nb, 256, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
         } else if (k == 1) {
-            k_jac_hash<8192><<<nb, 512, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out);
+            k_jac_hash<8192><<<nb, 512, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
         } else if (k == 2) {
-            k_jac_hash<16384><<<nb, 1024, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out);
+            k_jac_hash<16384><<<nb, 1024, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
         } else if (k == 3) {
-            k_jac_hash<32768><<<nb, 1024, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out);
+            k_jac_hash<32768><<<nb, 1024, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
         } else {
             // bitmaps in batches of rows (<= 1 GiB of bits at a time)
             const int64_t words = (n + 31) / 32;
@@ -487,13 +494,13 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts) {
                     ip, ix, grow, (int32_t)g0, words, bm);
                 if (tb[1] > tb[0])
                     k_jac_bitmap<<<(unsigned)(tb[1] - tb[0]), 1024, 0, st>>>(
-                        ip, ix, rev, ntask, trow, ti, tslot, tb[0], (int32_t)g0, words, bm, out);
+                        ip, ix, rev, ntask, trow, ti, tslot, tb[0], (int32_t)g0, words, bm, out, counts);
                 GS_HIP(hipGetLastError());
             }
         }
         GS_HIP(hipGetLastError());
     }
-    prof_end(c, t0, "jaccard", algo);
+    prof_end(c, t0, counts ? "common_neighbors" : "jaccard", algo);
 }
 
 }  // namespace gs

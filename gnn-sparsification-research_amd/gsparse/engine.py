@@ -219,6 +219,36 @@ class Engine:
         self.er_solve(0, k, max_cg_iters, cg_tol, bt)
         return self.er_scores(0, k, True)
 
+    # -- topology analytics (compute_topology_metrics, metrics.py:445-520) ----
+    def common_neighbors(self, out=None):
+        """gs_common_neighbors: |N(u) ∩ N(v)| per CSR entry (symmetric graph)."""
+        o, loc = self._out(0, self.nnz, out)
+        self.ctx.call("gs_common_neighbors", ptr(o), loc)
+        return o
+
+    def clustering(self, per_node: bool = False):
+        """gs_clustering: nx.average_clustering of the resident (symmetric,
+        self-loop-free) graph, bit-identical; optionally the per-node values."""
+        avg = ctypes.c_double(0.0)
+        cv = np.empty(max(self.n, 1), dtype=np.float64) if per_node else None
+        self.ctx.call("gs_clustering", ctypes.byref(avg), ptr(cv) if cv is not None else None,
+                      GS_HOST)
+        return (avg.value, cv[: self.n]) if per_node else avg.value
+
+    def components(self):
+        """gs_components: (labels = smallest node id per component, count, largest)."""
+        lab = np.empty(max(self.n, 1), dtype=np.int32)
+        cnt, big = ctypes.c_int64(0), ctypes.c_int64(0)
+        self.ctx.call("gs_components", ptr(lab), GS_HOST, ctypes.byref(cnt), ctypes.byref(big))
+        return lab[: self.n], cnt.value, big.value
+
+    def fiedler(self, tol: float = 1e-12, max_iter: int = 300):
+        """gs_fiedler: algebraic connectivity of the (connected) resident graph."""
+        v, it = ctypes.c_double(0.0), ctypes.c_int32(0)
+        self.ctx.call("gs_fiedler", float(tol), int(max_iter), ctypes.byref(v), ctypes.byref(it))
+        self.fiedler_iterations = it.value
+        return v.value
+
     # -- selection ------------------------------------------------------------
     def exact_er(self, out=None):
         """calculate_effective_resistance_scores (metrics.py:124-175) -- gs_exact_er:

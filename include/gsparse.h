@@ -166,12 +166,36 @@ int gs_metric_backbone_part(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *sr
 
 /* Exact effective resistance of the resident (symmetric) graph, one score per
  * CSR entry.  Replaces calculate_effective_resistance_scores (metrics.py:124-175:
- * dense pinv of L + 1e-10 I).  Computed as (M^-1)_uu + (M^-1)_vv - 2 (M^-1)_uv with
- * M = L + sum_C J_C/|C| (one lift per connected component), M^-1 by fp64-MFMA
- * Newton-Schulz; max(., 1e-10) as the reference clamps.  Dense: n <= 32768
- * (GS_EUNSUPPORTED above, and for a directed adjacency).  *iterations (may be
- * NULL) receives the Newton-Schulz step count. */
+ * dense pinv of L + 1e-10 I).  Computed as G_uu + G_vv - 2 G_uv with G the
+ * inverse of the grounded Laplacian M (one ground node per connected
+ * component, its row/column read as zero), G from a blocked fp64-MFMA Cholesky
+ * M = L L^T and L^-1 (GSPARSE_XER_METHOD=ns: Newton-Schulz); max(., 1e-10) as
+ * the reference clamps.  Dense: n <= 32768 (GS_EUNSUPPORTED above, and for a
+ * directed adjacency).  *iterations (may be NULL) receives the number of 64-row
+ * blocks (Cholesky) or Newton-Schulz steps. */
 int gs_exact_er(gs_ctx *ctx, double *out, int out_loc, int32_t *iterations);
+
+/* ---- compute_topology_metrics (metrics.py:445-520) on the resident graph ----
+ * The resident graph must be symmetric; the clustering and the counts expect
+ * it self-loop-free (NetworkX drops v from its own neighbour set).
+ *
+ * |N(u) ∩ N(v)| per CSR entry (exact integers as float64). */
+int gs_common_neighbors(gs_ctx *ctx, double *out, int out_loc);
+/* nx.average_clustering in NetworkX's operation order (bit-identical):
+ * c_v = 0 if t == 0 else t / (d (d - 1)), t = sum of the counts of v's entries,
+ * summed left to right from 0 in node order, / n.  per_node (may be NULL,
+ * location per_loc) receives c_v. */
+int gs_clustering(gs_ctx *ctx, double *avg, double *per_node, int per_loc);
+/* Connected components (nx.connected_components): labels[u] = smallest node id
+ * of u's component (may be NULL), *count, *largest (size of the largest). */
+int gs_components(gs_ctx *ctx, int32_t *labels, int labels_loc, int64_t *count,
+                  int64_t *largest);
+/* Algebraic connectivity (nx.algebraic_connectivity, weighted, unnormalised)
+ * of a connected resident graph, n <= 32768: 1 / lambda_max(P G P), G the
+ * grounded inverse of L (fp64-MFMA Cholesky), P = I - 11^T/n, by Lanczos with
+ * full reorthogonalisation until the Ritz value changes by <= tol (relative)
+ * or max_iter (<= 500) steps.  GS_EINVAL if the graph is not connected. */
+int gs_fiedler(gs_ctx *ctx, double tol, int32_t max_iter, double *value, int32_t *iterations);
 
 #ifdef __cplusplus
 }

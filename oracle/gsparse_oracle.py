@@ -350,3 +350,31 @@ def sampled_mask(scores, num_edges, retention_ratio, seed=42):
     mask = np.zeros(num_edges, dtype=bool)
     mask[selected] = True
     return mask
+
+
+def topology_metrics(adj):
+    """metrics.py:445-520, the reference's NetworkX calls restated (test oracle)."""
+    import networkx as nx
+    import scipy.sparse.linalg as spla_
+
+    n = adj.shape[0]
+    G = nx.from_scipy_sparse_array(adj)
+    num_edges = G.number_of_edges()
+    degrees = np.array([d for _, d in G.degree()])
+    avg_degree = degrees.mean() if len(degrees) > 0 else 0.0
+    clustering = nx.average_clustering(G)
+    components = list(nx.connected_components(G))
+    num_components = len(components)
+    largest = max(len(c) for c in components) if components else 0
+    ratio = largest / n if n > 0 else 0.0
+    ac = 0.0
+    if num_components == 1 and n > 1:
+        ac = nx.algebraic_connectivity(G, method="tracemin_lu")
+    elif num_components > 1:
+        lcc = max(components, key=len)
+        if len(lcc) > 1:
+            ac = nx.algebraic_connectivity(G.subgraph(lcc), method="tracemin_lu")
+    del spla_
+    return {"num_nodes": n, "num_edges": num_edges, "avg_degree": avg_degree,
+            "clustering_coefficient": clustering, "algebraic_connectivity": ac,
+            "num_connected_components": num_components, "largest_component_ratio": ratio}

@@ -574,3 +574,74 @@ def test_exact_er_empty_graph(gs):
 
     er = gs.calculate_effective_resistance_scores(sp.csr_matrix((5, 5)))
     assert er.shape == (0,)
+
+
+# ---- compute_topology_metrics (metrics.py:445-520), SURVEY 8(f) rank 4 -----
+def _topology_cases():
+    import scipy.sparse as sp
+
+    out = []
+    for name in ["karate_test", "cora_like", "roman2000", "rmat10", "star", "single_edge"]:
+        g = load_golden(name)
+        n = int(g["num_nodes"])
+        out.append((name, sp.csr_matrix((g["data"], g["indices"], g["indptr"]), shape=(n, n))))
+    # weighted, several components, self-loops, isolated nodes
+    rng = np.random.default_rng(7)
+    n = 900
+    r = rng.integers(0, 600, 2500)
+    c = (r + rng.integers(1, 40, 2500)) % 600
+    r = np.concatenate([r, np.arange(600, 850), [3, 17, 650]])
+    c = np.concatenate([c, np.arange(601, 851) % 850 + (np.arange(600, 850) >= 849) * 600,
+                        [3, 17, 650]])
+    w = rng.uniform(0.5, 2.0, len(r))
+    A = sp.coo_matrix((w, (r, c)), shape=(n, n)).tocsr()
+    A = (A + A.T).tocsr()
+    A.sum_duplicates()
+    out.append(("weighted_components_loops", A))
+    # directed, weighted (NetworkX keeps the later stored weight of a pair)
+    B = sp.random(300, 300, 0.03, random_state=3, format="csr")
+    B.data = rng.uniform(0.5, 2.0, B.nnz)
+    out.append(("directed_weighted", B))
+    return out
+
+
+@pytest.mark.parametrize("case", _topology_cases(), ids=lambda c: c[0])
+def test_topology_metrics_vs_networkx(gs, case):
+    """Exact fields (edges, degrees, clustering, components) identical to the
+    reference's NetworkX calls -- the clustering bit for bit; the algebraic
+    connectivity within 1e-6 relative (tracemin_lu stops at tol = 1e-8; the
+    device value is a Lanczos Ritz value on a Cholesky inverse)."""
+    _, adj = case
+    ref = O.topology_metrics(adj)
+    got = gs.compute_topology_metrics(adj)
+    for k in ["num_nodes", "num_edges", "num_connected_components"]:
+        assert got[k] == ref[k], k
+    for k in ["avg_degree", "clustering_coefficient", "largest_component_ratio"]:
+        assert bits_equal(np.array([got[k]]), np.array([ref[k]])), (k, got[k], ref[k])
+    np.testing.assert_allclose(got["algebraic_connectivity"], ref["algebraic_connectivity"],
+                               rtol=1e-6, atol=1e-14)
+
+
+def test_topology_preservation_and_counts(gs):
+    import scipy.sparse as sp
+
+    g = load_golden("karate_test")
+    n = int(g["num_nodes"])
+    adj = sp.csr_matrix((g["data"], g["indices"], g["indptr"]), shape=(n, n))
+    sp_, data = make(gs, g, with_x=False)
+    sd = sp_.sparsify("jaccard", 0.6)
+    ei = sd.edge_index.cpu().numpy()
+    sparse = sp.csr_matrix((np.ones(ei.shape[1]), (ei[0], ei[1])), shape=(n, n))
+    got = gs.compute_topology_preservation(adj, sparse)
+    ref_o, ref_s = O.topology_metrics(adj), O.topology_metrics(sparse)
+    assert got["component_change"] == ref_s["num_connected_components"] - ref_o["num_connected_components"]
+    assert got["edge_retention"] == ref_s["num_edges"] / ref_o["num_edges"]
+    # common-neighbour counts = the Jaccard numerators (A @ A on the 0/1 pattern)
+    from gsparse._lib import Context
+
+    ctx = Context()
+    ctx.set_graph_csr(n, adj.indptr, adj.indices, adj.data)
+    cnt = gs.engine.Engine(ctx).common_neighbors()
+    b = (adj > 0).astype(np.float64)
+    ref = np.asarray((b @ b)[adj.nonzero()]).ravel()
+    assert np.array_equal(cnt, ref)
