@@ -332,6 +332,84 @@ def cpu_baseline_exact_er(indptr, indices, data, n, max_n=4000):
                       f"({t:.2f}s measured, {total:.1f}s for the graph); BLAS threads={cores}"}
 
 
+def bench_topology(args, world, rank, local_rank, dev, dist):
+    """compute_topology_metrics (metrics.py:445-520) on the
+    Roman-like graph (default) or the Cora-size Chung-Lu graph (--xer-n 2708):
+    edges, degrees, clustering, components and the algebraic connectivity, one
+    step = the whole call.  CPU baseline: the reference's NetworkX calls
+    (oracle.topology_metrics).  Replicas only (per-graph analytics)."""
+    from gsparse import graphs
+    from gsparse.metrics import compute_topology_metrics
+
+    import scipy.sparse as sp
+
+    if args.xer_n == 2708:
+        n, ei, wl = 2_708, graphs.chung_lu(), "topology metrics, Cora-size Chung-Lu"
+    else:
+        n = args.xer_n or 22_662
+        ei = graphs.roman_like(n=n, m=int(n * 32_927 / 22_662), seed=0)
+        wl = f"topology metrics, Roman-like n={n}"
+    A = sp.csr_matrix((np.ones(ei.shape[1]), (ei[0], ei[1])), shape=(n, n))
+    A.sum_duplicates()
+    from gsparse.metrics import _scratch_context
+
+    ctx = _scratch_context()
+    for _ in range(args.warmup):
+        res = compute_topology_metrics(A)
+    torch.cuda.synchronize(dev)
+    ctx.profile(True)
+    ctx.profile_reset()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = compute_topology_metrics(A)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    roofline = None
+    if prof and "exact_er_dgemm" in prof:
+        p = prof["exact_er_dgemm"]
+        avg_ms = p["ms"] / p["launches"]
+        fl = p["bytes"] / p["launches"]
+        achieved = fl / (avg_ms * 1e-3) / 1e12
+        roofline = {"kernel": "k_chol_diag + k_tile_mm (grounded Cholesky and L^-1 for L^+)",
+                    "bound": "mfma", "achieved": round(achieved, 2), "peak": FP64_MFMA_PEAK_TFS,
+                    "unit": "TFLOP/s", "frac": round(achieved / FP64_MFMA_PEAK_TFS, 4),
+                    "traffic": None, "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": fl,
+                    "launches": p["launches"]}
+    result = {
+        "metric": "topology-metric calls/sec (compute_topology_metrics)",
+        "value": round(world * args.steps / elapsed, 3), "unit": "calls/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (stand-in graph of the config's size; datasets are not downloadable here)",
+        "config": {"workload": wl, "n": n, "E": int(A.nnz),
+                   "parallelism": f"{world} replicas" if world > 1 else "1 GPU",
+                   "result": {k: (float(v) if isinstance(v, (float, np.floating)) else int(v))
+                              for k, v in res.items()}},
+        "roofline": roofline,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import gsparse_oracle as O
+
+        t = time.perf_counter()
+        O.topology_metrics(A)
+        sec = time.perf_counter() - t
+        result["cpu_baseline"] = {"value": round(1.0 / sec, 4), "unit": "calls/s", "cores": 1,
+                                  "kind": "port",
+                                  "sample": "the reference's NetworkX calls (average_clustering, "
+                                            "connected_components, algebraic_connectivity "
+                                            f"tracemin_lu), one full call: {sec:.2f} s"}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def bench_exact_er(args, world, rank, local_rank, dev, dist):
     """calculate_effective_resistance_scores (metrics.py:124-175), the exact
     (dense) scorer the reference runs on small graphs: default Cora-size
@@ -439,7 +517,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="roman", choices=["roman", "rmat", "arxiv", "backbone", "exact_er"])
+    ap.add_argument("--workload", default="roman", choices=["roman", "rmat", "arxiv", "backbone", "exact_er", "topology"])
     ap.add_argument("--scale", type=int, default=22, help="R-MAT scale for --workload rmat")
     ap.add_argument("--bb-graph", default="rmat", choices=["rmat", "roman"],
                     help="graph of --workload backbone (R-MAT at --bb-scale, or Roman-like)")
@@ -479,6 +557,8 @@ def main():
         return bench_backbone(args, world, rank, local_rank, dev, dist)
     if args.workload == "exact_er":
         return bench_exact_er(args, world, rank, local_rank, dev, dist)
+    if args.workload == "topology":
+        return bench_topology(args, world, rank, local_rank, dev, dist)
 
     t_gen = time.perf_counter()
     if args.workload == "roman":
