@@ -410,6 +410,83 @@ def bench_topology(args, world, rank, local_rank, dev, dist):
         print(json.dumps(result), flush=True)
 
 
+def bench_geodesic(args, world, rank, local_rank, dev, dist):
+    """compute_geodesic_preservation (metrics.py:361-442) + verify_geodesic_preservation
+    (metric_backbone.py:144-225) on the Roman-like graph: 500 sampled pairs,
+    hop distances original vs the top-50% Jaccard subgraph, weighted (Jaccard
+    cost) distances original vs the same subgraph; one step = both calls.
+    CPU baseline: the reference's NetworkX calls (oracle.geodesic_preservation,
+    oracle.verify_geodesic).  Replicas only."""
+    from gsparse import graphs
+    from gsparse.data import Data
+    from gsparse.core import GraphSparsifier
+    from gsparse.metrics import compute_geodesic_preservation
+    from gsparse.metric_backbone import verify_geodesic_preservation
+
+    import scipy.sparse as sp
+
+    n = args.xer_n or 22_662
+    ei = graphs.roman_like(n=n, m=int(n * 32_927 / 22_662), seed=0)
+    data = Data(edge_index=torch.from_numpy(ei), num_nodes=n)
+    sp_ = GraphSparsifier(data, "cpu")
+    scores = sp_.compute_scores("jaccard")
+    cost = sp_._scores_to_cost(scores, "jaccard")
+    _, keep = sp_.sparsify("jaccard", 0.5, return_mask=True)
+    keep = keep.numpy()
+    ei_s = ei[:, keep]
+    sub = Data(edge_index=torch.from_numpy(ei_s), num_nodes=n)
+    A = sp.csr_matrix((np.ones(ei.shape[1]), (ei[0], ei[1])), shape=(n, n))
+    S = sp.csr_matrix((np.ones(ei_s.shape[1]), (ei_s[0], ei_s[1])), shape=(n, n))
+
+    def step():
+        a = compute_geodesic_preservation(A, S, n_samples=500)
+        b = verify_geodesic_preservation(data, sub, cost, cost[keep], n_samples=500)
+        return a, b
+
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    a, b = res
+    result = {
+        "metric": "geodesic-check calls/sec (compute_geodesic_preservation + verify_geodesic_preservation)",
+        "value": round(world * args.steps / elapsed, 3), "unit": "calls/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (stand-in graph of the config's size; datasets are not downloadable here)",
+        "config": {"workload": f"geodesic checks, Roman-like n={n}, top-50% Jaccard subgraph, 500 pairs",
+                   "n": n, "E": int(ei.shape[1]), "kept": int(keep.sum()),
+                   "parallelism": f"{world} replicas" if world > 1 else "1 GPU",
+                   "result": {"preservation_ratio": float(a["preservation_ratio"]),
+                              "violations": int(b["violations"]),
+                              "unreachable_backbone": int(b["unreachable_backbone"])}},
+        "roofline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import gsparse_oracle as O
+
+        t = time.perf_counter()
+        O.geodesic_preservation(A, S, n_samples=500)
+        O.verify_geodesic(ei, cost, ei_s, cost[keep], n, n_samples=500)
+        sec = time.perf_counter() - t
+        result["cpu_baseline"] = {"value": round(1.0 / sec, 4), "unit": "calls/s", "cores": 1,
+                                  "kind": "port",
+                                  "sample": "the reference's NetworkX calls (shortest_path_length "
+                                            f"hop + Dijkstra, 500 pairs each), one full step: {sec:.2f} s"}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def bench_exact_er(args, world, rank, local_rank, dev, dist):
     """calculate_effective_resistance_scores (metrics.py:124-175), the exact
     (dense) scorer the reference runs on small graphs: default Cora-size
@@ -517,7 +594,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="roman", choices=["roman", "rmat", "arxiv", "backbone", "exact_er", "topology"])
+    ap.add_argument("--workload", default="roman", choices=["roman", "rmat", "arxiv", "backbone", "exact_er", "topology", "geodesic"])
     ap.add_argument("--scale", type=int, default=22, help="R-MAT scale for --workload rmat")
     ap.add_argument("--bb-graph", default="rmat", choices=["rmat", "roman"],
                     help="graph of --workload backbone (R-MAT at --bb-scale, or Roman-like)")
@@ -559,6 +636,8 @@ def main():
         return bench_exact_er(args, world, rank, local_rank, dev, dist)
     if args.workload == "topology":
         return bench_topology(args, world, rank, local_rank, dev, dist)
+    if args.workload == "geodesic":
+        return bench_geodesic(args, world, rank, local_rank, dev, dist)
 
     t_gen = time.perf_counter()
     if args.workload == "roman":

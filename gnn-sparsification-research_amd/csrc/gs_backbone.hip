@@ -438,6 +438,46 @@ __global__ void __launch_bounds__(256) k_bb_landmarks(
     }
 }
 
+// Full searches for sampled node pairs (verify_geodesic_preservation,
+// compute_geodesic_preservation): one workgroup per distinct source, then the
+// exact distance of each of its targets (+inf when unreachable).
+__global__ void __launch_bounds__(256) k_bb_pairs(
+    const int64_t *__restrict__ gp, const int32_t *__restrict__ gi, const double *__restrict__ gw,
+    int64_t n, const int64_t *__restrict__ srcs, const int64_t *__restrict__ qptr,
+    const int64_t *__restrict__ qt, int64_t nsrc, double *__restrict__ out,
+    unsigned long long *__restrict__ dist_all, int32_t *__restrict__ qflag_all,
+    int32_t *__restrict__ fr_all, int32_t *__restrict__ touched_all) {
+    __shared__ int s_fcount, s_ncount, s_tcount;
+    __shared__ double s_inf;
+    unsigned long long *dist = dist_all + (int64_t)blockIdx.x * n;
+    int32_t *qflag = qflag_all + (int64_t)blockIdx.x * n;
+    int32_t *fa = fr_all + (int64_t)blockIdx.x * 2 * n;
+    int32_t *fb = fa + n;
+    int32_t *touched = touched_all + (int64_t)blockIdx.x * n;
+    unsigned long long relax = 0;
+    for (int64_t si = blockIdx.x; si < nsrc; si += gridDim.x) {
+        if (threadIdx.x == 0) {
+            s_fcount = 1;
+            s_ncount = 0;
+            s_tcount = 1;
+            s_inf = __builtin_inf();
+        }
+        __syncthreads();
+        bb_search(gp, gi, gw, (int32_t)srcs[si], s_inf, dist, qflag, fa, fb, touched, s_fcount,
+                  s_ncount, s_tcount, relax, [&] { __syncthreads(); });
+        for (int64_t q = qptr[si] + threadIdx.x; q < qptr[si + 1]; q += blockDim.x)
+            out[q] = __longlong_as_double((long long)dist[qt[q]]);
+        __syncthreads();
+        const int tc = s_tcount;
+        for (int t = threadIdx.x; t < tc; t += blockDim.x) {
+            const int32_t y = touched[t];
+            dist[y] = kInfBits;
+            qflag[y] = 0;
+        }
+        __syncthreads();
+    }
+}
+
 // Certificates for unresolved columns (state 0), each implying the exact
 // comparison w <= fl(d + eps) the reference makes (d = the fl left-fold
 // Dijkstra distance; fl sums of <= 2^31 terms are within 1e-9 relative of the
@@ -598,6 +638,48 @@ __global__ void k_bb_map(const int64_t *__restrict__ perm, const int64_t *__rest
     }
 }
 
+// G of metric_backbone.py:70-79 as a symmetric CSR: the columns with s < d in
+// the caller's ids (osrc/odst), keyed by the ids G is built in (src/dst), weight
+// the minimum over duplicates.  misc[0] is used as the unique-edge counter,
+// misc + 4 as the bad-input flag.
+static void bb_build_graph(gs_ctx *c, int64_t n, int64_t E, const int64_t *dsrc, const int64_t *ddst,
+                           const int64_t *osrc, const int64_t *odst, const double *dw,
+                           unsigned long long *misc, int64_t *&gp, int32_t *&gi, double *&gw) {
+    hipStream_t s = c->stream;
+    int *bad = (int *)(misc + 4);
+    uint64_t *keys = (uint64_t *)c->buf("bb_keys").ensure(8 * E);
+    int64_t *idx = (int64_t *)c->buf("bb_idx").ensure(8 * E);
+    k_bb_keys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, osrc, odst, dw, E, n, keys, idx,
+                                                     bad);
+    int hbad = 0;
+    GS_HIP(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    GS_CHECK(!(hbad & 1), GS_EINVAL, "edge_index entry out of range [0, %lld)", (long long)n);
+    GS_CHECK(!(hbad & 2), GS_EUNSUPPORTED,
+             "edge weights must be non-negative and not NaN (Dijkstra contract)");
+    sort_pairs_u64_i64(c, keys, idx, E, 64);
+    uint64_t *ukeys = (uint64_t *)c->buf("bb_ukeys").ensure(16 * E);
+    double *uw = (double *)c->buf("bb_uw").ensure(8 * E);
+    k_bb_unique<<<grid_for(E, 256, 8192), 256, 0, s>>>(keys, idx, dw, E, n, misc, ukeys, uw);
+    unsigned long long ucnt = 0;
+    GS_HIP(hipMemcpyAsync(&ucnt, misc, 8, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    int64_t cnt2 = 2 * (int64_t)ucnt;
+    // G as symmetric CSR sorted by (row, col): unique keys -> no ties in order
+    int64_t *pay = (int64_t *)c->buf("bb_pay").ensure(8 * (cnt2 + 1));
+    k_bb_sym_payload<<<grid_for(cnt2 + 1, 256, 8192), 256, 0, s>>>(cnt2, pay);
+    sort_pairs_u64_i64(c, ukeys, pay, cnt2, bits_for_bb((uint64_t)n * (uint64_t)n));
+    gp = (int64_t *)c->buf("bb_gp").ensure(8 * (n + 1));
+    gi = (int32_t *)c->buf("bb_gi").ensure(4 * (cnt2 + 1));
+    gw = (double *)c->buf("bb_gw").ensure(8 * (cnt2 + 1));
+    unsigned long long *deg = (unsigned long long *)c->buf("bb_flag").ensure(8 * (n + 1));
+    GS_HIP(hipMemsetAsync(deg, 0, 8 * (n + 1), s));
+    if (cnt2)
+        k_bb_gfill<<<grid_for(cnt2, 256, 8192), 256, 0, s>>>(ukeys, pay, uw, cnt2, n, gi, gw,
+                                                            deg);
+    exclusive_scan_i64(c, (const int64_t *)deg, gp, n + 1);
+}
+
 extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const int64_t *src,
                                        const int64_t *dst, const double *w, int loc, double eps,
                                        int part, int nparts, uint8_t *keep, int keep_loc,
@@ -672,38 +754,11 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
         int64_t relax = 0;
         hipEvent_t t0 = prof_begin(c);
         if (E > 0) {
-            int *bad = (int *)(misc + 4);
-            uint64_t *keys = (uint64_t *)b_keys.ensure(8 * E);
-            int64_t *idx = (int64_t *)b_idx.ensure(8 * E);
-            k_bb_keys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, osrc, odst, dw, E, n, keys, idx,
-                                                             bad);
-            int hbad = 0;
-            GS_HIP(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
-            GS_HIP(hipStreamSynchronize(s));
-            GS_CHECK(!(hbad & 1), GS_EINVAL, "edge_index entry out of range [0, %lld)", (long long)n);
-            GS_CHECK(!(hbad & 2), GS_EUNSUPPORTED,
-                     "edge weights must be non-negative and not NaN (Dijkstra contract)");
-            sort_pairs_u64_i64(c, keys, idx, E, 64);
-            uint64_t *ukeys = (uint64_t *)b_ukeys.ensure(16 * E);
-            double *uw = (double *)b_uw.ensure(8 * E);
-            k_bb_unique<<<grid_for(E, 256, 8192), 256, 0, s>>>(keys, idx, dw, E, n, misc, ukeys, uw);
-            unsigned long long ucnt = 0;
-            GS_HIP(hipMemcpyAsync(&ucnt, misc, 8, hipMemcpyDeviceToHost, s));
-            GS_HIP(hipStreamSynchronize(s));
-            int64_t cnt2 = 2 * (int64_t)ucnt;
-            // G as symmetric CSR sorted by (row, col): unique keys -> no ties in order
-            int64_t *pay = (int64_t *)b_pay.ensure(8 * (cnt2 + 1));
-            k_bb_sym_payload<<<grid_for(cnt2 + 1, 256, 8192), 256, 0, s>>>(cnt2, pay);
-            sort_pairs_u64_i64(c, ukeys, pay, cnt2, bits_for_bb((uint64_t)n * (uint64_t)n));
-            int64_t *gp = (int64_t *)b_gp.ensure(8 * (n + 1));
-            int32_t *gi = (int32_t *)b_gi.ensure(4 * (cnt2 + 1));
-            double *gw = (double *)b_gw.ensure(8 * (cnt2 + 1));
+            int64_t *gp;
+            int32_t *gi;
+            double *gw;
+            bb_build_graph(c, n, E, dsrc, ddst, osrc, odst, dw, misc, gp, gi, gw);
             unsigned long long *deg = (unsigned long long *)b_flag.ensure(8 * (n + 1));
-            GS_HIP(hipMemsetAsync(deg, 0, 8 * (n + 1), s));
-            if (cnt2)
-                k_bb_gfill<<<grid_for(cnt2, 256, 8192), 256, 0, s>>>(ukeys, pay, uw, cnt2, n, gi, gw,
-                                                                    deg);
-            exclusive_scan_i64(c, (const int64_t *)deg, gp, n + 1);
             // columns grouped by source row (stable: radix sort is stable)
             uint64_t *okeys = (uint64_t *)b_okeys.ensure(8 * E);
             int64_t *order = (int64_t *)b_order.ensure(8 * E);
@@ -817,4 +872,79 @@ extern "C" int gs_metric_backbone(gs_ctx *c, int64_t n, int64_t E, const int64_t
                                   const int64_t *dst, const double *w, int loc, double eps,
                                   uint8_t *keep, int keep_loc, int64_t *n_relax) {
     return gs_metric_backbone_part(c, n, E, src, dst, w, loc, eps, 0, 1, keep, keep_loc, n_relax);
+}
+
+extern "C" int gs_pair_distances(gs_ctx *c, int64_t n, int64_t E, const int64_t *src,
+                                 const int64_t *dst, const double *w, int loc, int64_t nq,
+                                 const int64_t *qs, const int64_t *qt, double *out) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        GS_CHECK(n >= 0 && E >= 0 && nq >= 0, GS_EINVAL, "negative n/E/nq");
+        GS_CHECK(n < (int64_t(1) << 31), GS_EUNSUPPORTED, "n >= 2^31");
+        GS_CHECK(nq == 0 || (qs && qt && out), GS_EINVAL, "null query arrays");
+        GS_HIP(hipSetDevice(c->device));
+        hipStream_t s = c->stream;
+        if (nq == 0) return;
+        // queries (host) grouped by source, in a stable order
+        std::vector<int64_t> ord((size_t)nq);
+        for (int64_t q = 0; q < nq; ++q) {
+            GS_CHECK(qs[q] >= 0 && qs[q] < n && qt[q] >= 0 && qt[q] < n, GS_EINVAL,
+                     "query %lld out of range [0, %lld)", (long long)q, (long long)n);
+            ord[(size_t)q] = q;
+        }
+        std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return qs[a] < qs[b]; });
+        std::vector<int64_t> srcs, qptr, tq((size_t)nq);
+        for (int64_t i = 0; i < nq; ++i) {
+            const int64_t q = ord[(size_t)i];
+            if (srcs.empty() || srcs.back() != qs[q]) {
+                srcs.push_back(qs[q]);
+                qptr.push_back(i);
+            }
+            tq[(size_t)i] = qt[q];
+        }
+        qptr.push_back(nq);
+        const int64_t nsrc = (int64_t)srcs.size();
+        std::vector<double> res((size_t)nq, __builtin_inf());
+        if (E > 0) {
+            const int64_t *dsrc = (const int64_t *)to_device(c, c->buf("bp_src"), src, 8 * E, loc);
+            const int64_t *ddst = (const int64_t *)to_device(c, c->buf("bp_dst"), dst, 8 * E, loc);
+            const double *dw;
+            if (w) {
+                dw = (const double *)to_device(c, c->buf("bp_w"), w, 8 * E, loc);
+            } else {  // unweighted: hop counts (sums of 1.0 are exact)
+                std::vector<double> ones((size_t)E, 1.0);
+                double *d1 = (double *)c->buf("bp_w").ensure(8 * E);
+                GS_HIP(hipMemcpy(d1, ones.data(), 8 * E, hipMemcpyHostToDevice));
+                dw = d1;
+            }
+            auto *misc = (unsigned long long *)c->buf("bp_misc").ensure(64);
+            GS_HIP(hipMemsetAsync(misc, 0, 64, s));
+            int64_t *gp;
+            int32_t *gi;
+            double *gw;
+            bb_build_graph(c, n, E, dsrc, ddst, dsrc, ddst, dw, misc, gp, gi, gw);
+            int64_t *d_src = (int64_t *)c->buf("bp_srcs").ensure(8 * nsrc);
+            int64_t *d_ptr = (int64_t *)c->buf("bp_qptr").ensure(8 * (nsrc + 1));
+            int64_t *d_tq = (int64_t *)c->buf("bp_tq").ensure(8 * nq);
+            double *d_out = (double *)c->buf("bp_out").ensure(8 * nq);
+            GS_HIP(hipMemcpyAsync(d_src, srcs.data(), 8 * nsrc, hipMemcpyHostToDevice, s));
+            GS_HIP(hipMemcpyAsync(d_ptr, qptr.data(), 8 * (nsrc + 1), hipMemcpyHostToDevice, s));
+            GS_HIP(hipMemcpyAsync(d_tq, tq.data(), 8 * nq, hipMemcpyHostToDevice, s));
+            const int64_t slabs = nsrc < 256 ? nsrc : 256;
+            auto *dist = (unsigned long long *)c->buf("bb_dist").ensure(8 * slabs * n);
+            auto *qflag = (int32_t *)c->buf("bb_qflag").ensure(4 * slabs * n);
+            auto *fr = (int32_t *)c->buf("bb_fr").ensure(8 * slabs * n);
+            auto *touched = (int32_t *)c->buf("bb_touched").ensure(4 * slabs * n);
+            k_bb_fill_u64<<<grid_for(slabs * n, 256, 65536), 256, 0, s>>>(dist, slabs * n, kInfBits);
+            GS_HIP(hipMemsetAsync(qflag, 0, 4 * slabs * n, s));
+            k_bb_pairs<<<(unsigned)slabs, 256, 0, s>>>(gp, gi, gw, n, d_src, d_ptr, d_tq, nsrc, d_out,
+                                                       dist, qflag, fr, touched);
+            GS_HIP(hipGetLastError());
+            std::vector<double> hout((size_t)nq);
+            GS_HIP(hipMemcpyAsync(hout.data(), d_out, 8 * nq, hipMemcpyDeviceToHost, s));
+            GS_HIP(hipStreamSynchronize(s));
+            for (int64_t i = 0; i < nq; ++i) res[(size_t)ord[(size_t)i]] = hout[(size_t)i];
+        }
+        for (int64_t q = 0; q < nq; ++q) out[q] = qs[q] == qt[q] ? 0.0 : res[(size_t)q];
+    });
 }

@@ -64,6 +64,7 @@ SIGNATURES = {
     "gs_metric_backbone_part": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _int, _f64, _int, _int,
                                        _vp, _int, ctypes.POINTER(_i64)]),
     "gs_exact_er": (_int, [_vp, _vp, _int, ctypes.POINTER(_i32)]),
+    "gs_pair_distances": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _int, _i64, _vp, _vp, _vp]),
     "gs_common_neighbors": (_int, [_vp, _vp, _int]),
     "gs_clustering": (_int, [_vp, ctypes.POINTER(_f64), _vp, _int]),
     "gs_components": (_int, [_vp, _vp, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),

@@ -129,9 +129,65 @@ def calculate_feature_cosine_scores(adj: sp.csr_matrix, features: np.ndarray) ->
     return _unpermute(eng.feature_cosine(features), perm)
 
 
-def compute_geodesic_preservation(*args, **kwargs):  # pragma: no cover - analysis helper
-    raise NotImplementedError("NetworkX geodesic analysis is outside the accelerated path "
-                              "(SURVEY §8(f)); use the reference implementation")
+def compute_geodesic_preservation(
+    original_adj: sp.csr_matrix,
+    sparse_adj: sp.csr_matrix,
+    n_samples: int = 500,
+    seed: int = 42,
+) -> Dict:
+    """Geodesic (hop-distance) preservation between sampled node pairs
+    (metrics.py:361-442): the reference's RNG calls and bookkeeping, the hop
+    distances of ``nx.from_scipy_sparse_array``'s graphs from gs_pair_distances
+    (exact, unit weights)."""
+    from .metric_backbone import pair_distances
+
+    n = original_adj.shape[0]
+    rng = np.random.default_rng(seed)
+    pairs = set()
+    max_attempts = n_samples * 10
+    attempts = 0
+    while len(pairs) < n_samples and attempts < max_attempts:
+        u, v = rng.integers(0, n, size=2)
+        if u != v:
+            pairs.add((min(u, v), max(u, v)))
+        attempts += 1
+    pairs = list(pairs)
+
+    def hops(adj):
+        coo = sp.coo_matrix(adj)
+        r = coo.row.astype(np.int64)
+        c = coo.col.astype(np.int64)
+        ei = np.stack([np.concatenate([r, c]), np.concatenate([c, r])])
+        return pair_distances(ei, adj.shape[0], None, pairs) if pairs else np.zeros(0)
+
+    d_o, d_s = hops(original_adj), hops(sparse_adj)
+    preserved = 0
+    increased = 0
+    disconnected = 0
+    distance_increases = []
+    for a, b in zip(d_o, d_s):
+        if np.isinf(a):
+            continue  # already disconnected in the original
+        if np.isinf(b):
+            disconnected += 1
+            continue
+        d_orig, d_sparse = int(a), int(b)
+        if d_sparse == d_orig:
+            preserved += 1
+        else:
+            increased += 1
+            distance_increases.append(d_sparse - d_orig)
+    total_valid = preserved + increased + disconnected
+    preservation_ratio = preserved / total_valid if total_valid > 0 else 0.0
+    return {
+        "preservation_ratio": preservation_ratio,
+        "pairs_tested": len(pairs),
+        "preserved_count": preserved,
+        "increased_count": increased,
+        "disconnected_count": disconnected,
+        "avg_distance_increase": np.mean(distance_increases) if distance_increases else 0.0,
+        "max_distance_increase": max(distance_increases) if distance_increases else 0,
+    }
 
 
 def _nx_graph_arrays(adj):

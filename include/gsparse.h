@@ -164,6 +164,18 @@ int gs_metric_backbone_part(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *sr
                             const int64_t *dst, const double *w, int loc, double eps, int part,
                             int nparts, uint8_t *keep, int keep_loc, int64_t *n_relax);
 
+/* Exact shortest-path distances for nq node pairs (qs[q], qt[q]) (host arrays;
+ * out host) in the graph metric_backbone.py:70-79 builds from the columns
+ * (src, dst, w): undirected, the columns with src < dst, weight the minimum
+ * over duplicates; w == NULL: unit weights (hop counts).  +inf when
+ * unreachable; 0 when qs == qt.  Bit-identical to NetworkX Dijkstra's
+ * left-fold path sums.  Replaces the nx.shortest_path_length calls of
+ * verify_geodesic_preservation (metric_backbone.py:144-225) and
+ * compute_geodesic_preservation (metrics.py:361-442). */
+int gs_pair_distances(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src, const int64_t *dst,
+                      const double *w, int loc, int64_t nq, const int64_t *qs, const int64_t *qt,
+                      double *out);
+
 /* Exact effective resistance of the resident (symmetric) graph, one score per
  * CSR entry.  Replaces calculate_effective_resistance_scores (metrics.py:124-175:
  * dense pinv of L + 1e-10 I).  Computed as G_uu + G_vv - 2 G_uv with G the

@@ -378,3 +378,83 @@ def topology_metrics(adj):
     return {"num_nodes": n, "num_edges": num_edges, "avg_degree": avg_degree,
             "clustering_coefficient": clustering, "algebraic_connectivity": ac,
             "num_connected_components": num_components, "largest_component_ratio": ratio}
+
+
+def geodesic_preservation(original_adj, sparse_adj, n_samples=500, seed=42):
+    """metrics.py:361-442 restated with the reference's NetworkX calls (test oracle)."""
+    import networkx as nx
+
+    n = original_adj.shape[0]
+    rng = np.random.default_rng(seed)
+    G_orig = nx.from_scipy_sparse_array(original_adj)
+    G_sparse = nx.from_scipy_sparse_array(sparse_adj)
+    pairs = set()
+    max_attempts = n_samples * 10
+    attempts = 0
+    while len(pairs) < n_samples and attempts < max_attempts:
+        u, v = rng.integers(0, n, size=2)
+        if u != v:
+            pairs.add((min(u, v), max(u, v)))
+        attempts += 1
+    pairs = list(pairs)
+    preserved = increased = disconnected = 0
+    inc = []
+    for u, v in pairs:
+        try:
+            d_orig = nx.shortest_path_length(G_orig, u, v)
+        except nx.NetworkXNoPath:
+            continue
+        try:
+            d_sparse = nx.shortest_path_length(G_sparse, u, v)
+        except nx.NetworkXNoPath:
+            disconnected += 1
+            continue
+        if d_sparse == d_orig:
+            preserved += 1
+        else:
+            increased += 1
+            inc.append(d_sparse - d_orig)
+    total = preserved + increased + disconnected
+    return {"preservation_ratio": preserved / total if total > 0 else 0.0,
+            "pairs_tested": len(pairs), "preserved_count": preserved,
+            "increased_count": increased, "disconnected_count": disconnected,
+            "avg_distance_increase": np.mean(inc) if inc else 0.0,
+            "max_distance_increase": max(inc) if inc else 0}
+
+
+def verify_geodesic(ei_o, w_o, ei_s, w_s, n, n_samples=500, epsilon=1e-6, seed=42):
+    """metric_backbone.py:144-225 restated with the reference's NetworkX calls (test oracle)."""
+    import networkx as nx
+
+    def build(ei, w):
+        G = nx.Graph()
+        G.add_nodes_from(range(n))
+        for idx, (u, v) in enumerate(zip(ei[0], ei[1])):
+            if u < v:
+                x = w[idx]
+                if G.has_edge(u, v):
+                    G[u][v]["weight"] = min(G[u][v]["weight"], x)
+                else:
+                    G.add_edge(u, v, weight=x)
+        return G
+
+    Go, Gb = build(ei_o, w_o), build(ei_s, w_s)
+    rng = np.random.default_rng(seed)
+    pairs = set()
+    while len(pairs) < n_samples:
+        u, v = rng.integers(0, n, size=2)
+        if u != v:
+            pairs.add((min(u, v), max(u, v)))
+    pairs = list(pairs)
+    dists = []
+    for u, v in pairs:
+        try:
+            a = nx.shortest_path_length(Go, u, v, weight="weight")
+        except nx.NetworkXNoPath:
+            a = float("inf")
+        try:
+            b = nx.shortest_path_length(Gb, u, v, weight="weight")
+        except nx.NetworkXNoPath:
+            b = float("inf")
+        dists.append((float(a), float(b)))
+    return pairs, dists

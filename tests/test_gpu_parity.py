@@ -645,3 +645,66 @@ def test_topology_preservation_and_counts(gs):
     b = (adj > 0).astype(np.float64)
     ref = np.asarray((b @ b)[adj.nonzero()]).ravel()
     assert np.array_equal(cnt, ref)
+
+
+# ---- sampled-pair shortest paths (compute_geodesic_preservation, verify_geodesic_preservation)
+@pytest.mark.parametrize("name", ["karate_test", "cora_like", "roman2000", "rmat10"])
+def test_geodesic_analytics_vs_networkx(gs, name):
+    """The same sampled pairs, hop distances and weighted Dijkstra distances as the
+    reference's NetworkX calls -- equal, not close: every distance is an exact
+    left-fold path sum."""
+    import scipy.sparse as sp
+
+    g = load_golden(name)
+    n = int(g["num_nodes"])
+    adj = sp.csr_matrix((g["data"], g["indices"], g["indptr"]), shape=(n, n))
+    sp_, data = make(gs, g, with_x=False)
+    sd, mask = sp_.sparsify("jaccard", 0.5, return_mask=True)
+    ei_s = sd.edge_index.cpu().numpy()
+    sparse = sp.csr_matrix((np.ones(ei_s.shape[1]), (ei_s[0], ei_s[1])), shape=(n, n))
+    got = gs.compute_geodesic_preservation(adj, sparse, n_samples=300)
+    ref = O.geodesic_preservation(adj, sparse, n_samples=300)
+    assert got == ref
+    # weighted: the metric backbone of the Jaccard costs vs the whole graph
+    ei = g["edge_index"]
+    cost = g["cost_jaccard"]
+    bd, st = gs.compute_metric_backbone(data, cost, epsilon=1e-9, verbose=False)
+    keep = st["keep_mask"]
+    pairs, dists = O.verify_geodesic(ei, cost, ei[:, keep], cost[keep], n, n_samples=300)
+    from gsparse.metric_backbone import pair_distances
+
+    assert len(pairs) == 300
+    d_o = pair_distances(ei, n, cost, pairs)
+    d_b = pair_distances(ei[:, keep], n, cost[keep], pairs)
+    assert np.array_equal(d_o, np.array([a for a, _ in dists]))
+    assert np.array_equal(d_b, np.array([b for _, b in dists]))
+    from gsparse.metric_backbone import verify_geodesic_preservation
+
+    res = verify_geodesic_preservation(data, bd, cost, cost[keep], n_samples=300)
+    assert res["pairs_tested"] == len(pairs) and res["violations"] == 0
+
+
+@pytest.mark.parametrize("name", ["karate_test", "cora_like", "rmat10"])
+def test_geodesic_violations_vs_networkx(gs, name):
+    """A subgraph that is NOT the backbone (the top-50% Jaccard mask): the
+    violation / unreachable bookkeeping of metric_backbone.py:199-225 on the
+    oracle's NetworkX distances."""
+    from gsparse.metric_backbone import verify_geodesic_preservation
+
+    g = load_golden(name)
+    n = int(g["num_nodes"])
+    _, data = make(gs, g, with_x=False)
+    ei, cost = g["edge_index"], g["cost_jaccard"]
+    keep = g["mask_jaccard_0.5_0"]
+    sub = gs.Data(edge_index=torch.from_numpy(ei[:, keep]), num_nodes=n)
+    res = verify_geodesic_preservation(data, sub, cost, cost[keep], n_samples=200)
+    pairs, dists = O.verify_geodesic(ei, cost, ei[:, keep], cost[keep], n, n_samples=200)
+    uo = sum(np.isinf(a) for a, _ in dists)
+    ub = sum((not np.isinf(a)) and np.isinf(b) for a, b in dists)
+    viol = [abs(a - b) for a, b in dists if not np.isinf(a) and not np.isinf(b) and abs(a - b) > 1e-6]
+    assert res["unreachable_original"] == uo and res["unreachable_backbone"] == ub
+    assert res["violations"] == len(viol) + ub
+    assert res["verified_equal"] == len(pairs) - uo - ub - len(viol)
+    if not ub:
+        assert res["max_violation"] == (max(viol) if viol else 0.0)
+    assert res["violations"] > 0
