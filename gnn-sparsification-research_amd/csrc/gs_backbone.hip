@@ -694,8 +694,7 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
         hipStream_t s = c->stream;
         // own buffers (the scorer scratch slots stay untouched)
 #define BB(name) DevBuf &b_##name = c->buf("bb_" #name)
-        BB(src); BB(dst); BB(w); BB(keys); BB(idx); BB(ukeys); BB(uw); BB(pay); BB(gp); BB(gi);
-        BB(gw); BB(okeys); BB(order); BB(optr); BB(state); BB(flag); BB(pos); BB(sources);
+        BB(src); BB(dst); BB(w); BB(okeys); BB(order); BB(optr); BB(state); BB(flag); BB(pos); BB(sources);
         BB(dist); BB(qflag); BB(fr); BB(touched); BB(misc); BB(keep); BB(lm); BB(land); BB(lcomp);
         BB(msrc); BB(mdst); BB(perm);
 #undef BB
@@ -912,9 +911,9 @@ extern "C" int gs_pair_distances(gs_ctx *c, int64_t n, int64_t E, const int64_t 
             if (w) {
                 dw = (const double *)to_device(c, c->buf("bp_w"), w, 8 * E, loc);
             } else {  // unweighted: hop counts (sums of 1.0 are exact)
-                std::vector<double> ones((size_t)E, 1.0);
                 double *d1 = (double *)c->buf("bp_w").ensure(8 * E);
-                GS_HIP(hipMemcpy(d1, ones.data(), 8 * E, hipMemcpyHostToDevice));
+                k_bb_fill_u64<<<grid_for(E, 256, 8192), 256, 0, s>>>(
+                    (unsigned long long *)d1, E, 0x3ff0000000000000ull);  // 1.0
                 dw = d1;
             }
             auto *misc = (unsigned long long *)c->buf("bp_misc").ensure(64);

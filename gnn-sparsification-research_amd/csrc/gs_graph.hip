@@ -124,6 +124,40 @@ __global__ void k_tsplit(const uint64_t *__restrict__ keys, int64_t nnz, int64_t
     }
 }
 
+// Canonical edge list (the loader's to_undirected + coalesce): keys of both
+// directions, dropped entries (self-loops when asked) keyed n*n so the sort
+// puts them last; sorted unique keys -> (row, col) int64.
+__global__ void k_pair_keys(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
+                            int64_t E, int64_t n, int both, int drop_loops,
+                            uint64_t *__restrict__ keys, int *__restrict__ bad) {
+    const uint64_t un = (uint64_t)n, drop = un * un;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t s = src[i], d = dst[i];
+        if (s < 0 || s >= n || d < 0 || d >= n) {
+            atomicOr(bad, 1);
+            s = d = 0;
+        }
+        const bool gone = drop_loops && s == d;
+        keys[i] = gone ? drop : (uint64_t)s * un + (uint64_t)d;
+        if (both) keys[E + i] = gone ? drop : (uint64_t)d * un + (uint64_t)s;
+    }
+}
+
+__global__ void k_compact_pairs(const uint64_t *__restrict__ keys, const int64_t *__restrict__ flag,
+                                const int64_t *__restrict__ pos, int64_t E, int64_t n,
+                                int64_t *__restrict__ row, int64_t *__restrict__ col) {
+    const uint64_t un = (uint64_t)n;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t k = keys[i];
+        if (flag[i] && k < un * un) {
+            row[pos[i]] = (int64_t)(k / un);
+            col[pos[i]] = (int64_t)(k % un);
+        }
+    }
+}
+
 static void build_indptr_from_rows(gs_ctx *c) {
     Graph &g = c->g;
     int64_t n = g.n, nnz = g.nnz;
@@ -290,6 +324,59 @@ int gs_graph_from_csr(gs_ctx *c, int64_t n, int64_t nnz, const int64_t *indptr,
             k_rows_from_indptr<<<grid_for(n, 256, 8192), 256, 0, c->stream>>>(ip, n,
                                                                               g.rows.as<int32_t>());
         finish_graph(c);
+    });
+}
+
+int gs_coalesce_edges(gs_ctx *c, int64_t n, int64_t E, const int64_t *src, const int64_t *dst,
+                      int undirected, int remove_self_loops, int64_t *out_src, int64_t *out_dst,
+                      int64_t *out_E, int loc) {
+    return guard([&] {
+        GS_CHECK(c && out_E, GS_EINVAL, "null context/out_E");
+        GS_CHECK(n >= 0 && E >= 0, GS_EINVAL, "negative n/E");
+        GS_CHECK(n < (int64_t(1) << 31), GS_EUNSUPPORTED, "n >= 2^31 nodes");
+        GS_HIP(hipSetDevice(c->device));
+        const int64_t cap = *out_E, M = undirected ? 2 * E : E;
+        *out_E = 0;
+        if (E == 0) return;
+        const int64_t *dsrc = (const int64_t *)to_device(c, c->inbuf, src, sizeof(int64_t) * E, loc);
+        const int64_t *ddst = (const int64_t *)to_device(c, c->inbuf2, dst, sizeof(int64_t) * E, loc);
+        int *bad = (int *)c->scratch[1].ensure(64);
+        GS_HIP(hipMemsetAsync(bad, 0, sizeof(int), c->stream));
+        uint64_t *keys = (uint64_t *)c->scratch[2].ensure(sizeof(uint64_t) * M);
+        k_pair_keys<<<grid_for(E, 256, 8192), 256, 0, c->stream>>>(
+            dsrc, ddst, E, n, undirected ? 1 : 0, remove_self_loops ? 1 : 0, keys, bad);
+        int hbad = 0;
+        GS_HIP(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        GS_HIP(hipStreamSynchronize(c->stream));
+        GS_CHECK(!hbad, GS_EINVAL, "edge_index entry out of range [0, %lld)", (long long)n);
+        const uint64_t un = (uint64_t)n;
+        sort_keys_u64(c, keys, M, bits_for(un * un));
+        int64_t *flag = (int64_t *)c->scratch[0].ensure(sizeof(int64_t) * M);
+        int64_t *pos = (int64_t *)c->scratch[1].ensure(sizeof(int64_t) * M + 64);
+        k_head_flags<<<grid_for(M, 256, 8192), 256, 0, c->stream>>>(keys, M, flag);
+        exclusive_scan_i64(c, flag, pos, M);
+        int64_t last[2];
+        uint64_t lastkey = 0;
+        GS_HIP(hipMemcpyAsync(&last[0], pos + M - 1, sizeof(int64_t), hipMemcpyDeviceToHost,
+                              c->stream));
+        GS_HIP(hipMemcpyAsync(&last[1], flag + M - 1, sizeof(int64_t), hipMemcpyDeviceToHost,
+                              c->stream));
+        GS_HIP(hipMemcpyAsync(&lastkey, keys + M - 1, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                              c->stream));
+        GS_HIP(hipStreamSynchronize(c->stream));
+        const int64_t m = last[0] + last[1] - (lastkey == un * un ? 1 : 0);
+        GS_CHECK(m <= cap, GS_EINVAL, "output capacity %lld < %lld edges", (long long)cap,
+                 (long long)m);
+        if (m > 0) {
+            int64_t *orow = (int64_t *)c->scratch[3].ensure(sizeof(int64_t) * 2 * m);
+            k_compact_pairs<<<grid_for(M, 256, 8192), 256, 0, c->stream>>>(keys, flag, pos, M, n,
+                                                                           orow, orow + m);
+            hipMemcpyKind kind = loc == GS_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+            GS_HIP(hipMemcpyAsync(out_src, orow, sizeof(int64_t) * m, kind, c->stream));
+            GS_HIP(hipMemcpyAsync(out_dst, orow + m, sizeof(int64_t) * m, kind, c->stream));
+            GS_HIP(hipStreamSynchronize(c->stream));
+        }
+        *out_E = m;
     });
 }
 

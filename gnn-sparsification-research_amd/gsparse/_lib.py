@@ -40,6 +40,7 @@ SIGNATURES = {
     "gs_profile_get": (_int, [_vp, _int, ctypes.c_char_p, _int, ctypes.POINTER(_i64),
                               ctypes.POINTER(_f64), ctypes.POINTER(_f64)]),
     "gs_graph_from_edge_index": (_int, [_vp, _i64, _i64, _vp, _vp, _int]),
+    "gs_coalesce_edges": (_int, [_vp, _i64, _i64, _vp, _vp, _int, _int, _vp, _vp, _vp, _int]),
     "gs_graph_from_csr": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _int]),
     "gs_graph_shape": (_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64), ctypes.POINTER(_int)]),
     "gs_graph_copy_csr": (_int, [_vp, _vp, _vp, _vp, _int]),

@@ -72,6 +72,14 @@ int gs_graph_from_edge_index(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *s
 int gs_graph_from_csr(gs_ctx *ctx, int64_t n, int64_t nnz, const int64_t *indptr,
                       const int32_t *indices, const double *data, int loc);
 int gs_graph_shape(gs_ctx *ctx, int64_t *n, int64_t *nnz, int *symmetric);
+/* Canonical edge list for the dataset loader (gsparse/loader.py, standing in
+ * for the reference's absent src/data; PyG's to_undirected + coalesce):
+ * undirected != 0 adds every reversed pair; remove_self_loops != 0 drops
+ * u == v; the result is sorted by (row, col) with duplicates removed.
+ * *out_E: capacity on entry (2E suffices), edge count on return. */
+int gs_coalesce_edges(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src, const int64_t *dst,
+                      int undirected, int remove_self_loops, int64_t *out_src, int64_t *out_dst,
+                      int64_t *out_E, int loc);
 int gs_graph_copy_csr(gs_ctx *ctx, int64_t *indptr, int32_t *indices, double *data, int loc);
 
 /* ---- scorers: out[e - e0] for CSR entries e in [e0, e1) ------------------ */

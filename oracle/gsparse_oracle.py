@@ -458,3 +458,20 @@ def verify_geodesic(ei_o, w_o, ei_s, w_s, n, n_samples=500, epsilon=1e-6, seed=4
             b = float("inf")
         dists.append((float(a), float(b)))
     return pairs, dists
+
+
+def coalesce(edge_index, n, undirected=True, remove_self_loops=False):
+    """The loader's canonical edge list (test oracle; PyG's to_undirected +
+    coalesce, whose published algorithm is: cat([row, col], [col, row]), sort
+    by row * n + col, drop repeats).  The reference's own src/data is absent,
+    so this is pinned only by that published behaviour: parity unpinned
+    against the reference itself."""
+    ei = np.asarray(edge_index, dtype=np.int64).reshape(2, -1)
+    r, c = ei[0], ei[1]
+    if undirected:
+        r, c = np.concatenate([r, c]), np.concatenate([c, r])
+    if remove_self_loops:
+        keep = r != c
+        r, c = r[keep], c[keep]
+    keys = np.unique(r * np.int64(n) + c)
+    return np.stack([keys // n, keys % n]).astype(np.int64)
