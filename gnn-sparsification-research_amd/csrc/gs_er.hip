@@ -1245,9 +1245,9 @@ __device__ __forceinline__ void res_spmv(const ResArgs &A, const double *p, doub
         }
 #pragma unroll
         for (int i = 0; i < RB; ++i)
-            if (ok[i]) {
-                q[row[i]] = acc[i];
+            if (ok[i]) {  // rows mirrored in LDS live only there (chunk tails: copied below)
                 if (row[i] < ql) sq[row[i]] = acc[i];
+                else q[row[i]] = acc[i];
             }
     }
 }
@@ -1290,8 +1290,8 @@ __device__ __forceinline__ void res_spmv_ell(const ResArgs &A, const double *p, 
                 acc = col[i][k] >= 0 ? qn : acc;
             }
             if (ok[i]) {
-                q[row[i]] = acc;
                 if (row[i] < ql) sq[row[i]] = acc;
+                else q[row[i]] = acc;
             }
         }
     }
@@ -1385,7 +1385,9 @@ __global__ void __launch_bounds__(kResThreads) k_cg_resident(ResArgs A, ChunkArg
             if (it == 0) {
                 for (int64_t i = tid; i < n; i += kResThreads) p[i] = r[i];
             } else {
-                constexpr int U = 4;
+                // 8 rows per thread in flight (Roman: 82.6 vs 86.8 ms of workgroup 0's
+                // 465 / 470 ms with 4)
+                constexpr int U = 8;
                 for (int64_t i0 = tid; i0 < n; i0 += kResThreads * U) {
                     double po[U], rv[U], xv[U];
 #pragma unroll
@@ -1415,6 +1417,14 @@ __global__ void __launch_bounds__(kResThreads) k_cg_resident(ResArgs A, ChunkArg
             __syncthreads();
             lap(1);
             chain_dot(p, q, true);
+            // the chunk tails (< 32 rows past each chunk's chains) are read from the q slot
+            // by the finish and the r update: copy the LDS-only ones there
+            for (int k = tid; k < nchains; k += kResThreads) {
+                int64_t a, L, e32;
+                chain_geom(k, a, L, e32);
+                const int64_t rw = e32 + (k & 31);
+                if (rw < L && rw < ql) q[rw] = sq[rw];
+            }
             lap(2);
             const double pq = finish(p, q);
             const double alpha = rho_cur / pq;
