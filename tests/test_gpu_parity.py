@@ -82,8 +82,14 @@ def chunked_er():
     # the same graph with every 7th edge doubled: multiplicity-2 entries, so the
     # resident solver's unit-weight SELL form does not apply
     dup = np.concatenate([ei, ei[:, ::7]], axis=1)
+    # unit weights with a few rows wider than the SpMV's first 8 entries (its tail loop)
+    rng = np.random.default_rng(11)
+    extra = [(h, int(v)) for h, k in ((5, 40), (6001, 13), (11990, 9)) for v in rng.choice(n, k, replace=False)
+             if v != h]
+    ex = np.array(extra, dtype=np.int64).T
+    hub = O.coalesce(np.concatenate([ei, ex], axis=1), n)
     out = {}
-    for gname, e in (("unit", ei), ("dup", dup)):
+    for gname, e in (("unit", ei), ("dup", dup), ("hub", hub)):
         ip, ix, d = O.canonical_csr(e, n)
         out[gname] = (e, {t: O.approx_er(ip, ix, d, n, epsilon=0.9, max_cg_iters=60, impl="c",
                                          blas_threads=t) for t in (3, 8)})
@@ -106,7 +112,7 @@ def chunked_er():
                               "m4-weighted-sell", "m4-weighted-ell", "m4-slices-global",
                               "m4-rb4w4", "m4-rb4w4-weighted"])
 @pytest.mark.parametrize("threads", [3, 8])
-@pytest.mark.parametrize("graph", ["unit", "dup"])
+@pytest.mark.parametrize("graph", ["unit", "dup", "hub"])
 def test_approx_er_blas_chunks_vs_oracle(gs, chunked_er, graph, threads, env, monkeypatch):
     """T-chunk ddot order (T = 3, 8) in every CG mode, bit-identical to the oracle."""
     for k_, v in env.items():
