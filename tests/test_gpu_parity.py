@@ -714,3 +714,37 @@ def test_geodesic_violations_vs_networkx(gs, name):
     if not ub:
         assert res["max_violation"] == (max(viol) if viol else 0.0)
     assert res["violations"] > 0
+
+
+@pytest.mark.parametrize("threads", ["256", "1024"])
+@pytest.mark.parametrize("S", ["2", "4", "8"])
+def test_backbone_multi_source_searches(gs, S, threads, monkeypatch):
+    """S sources per workgroup (GSPARSE_BB_MULTI, interleaved labels): the keep
+    masks of the reference goldens, of the RMAT-12 oracle, and of the
+    single-source searches with the certificates off (most columns searched)."""
+    from gsparse import graphs
+    from gsparse.metric_backbone import backbone_mask
+
+    monkeypatch.setenv("GSPARSE_BB_THREADS", threads)
+    monkeypatch.setenv("GSPARSE_BB_MULTI", S)
+    for name in ["karate_test", "directed_dup", "rmat10", "roman2000", "cora_like", "star"]:
+        g = load_golden(name)
+        _, data = make(gs, g, with_x=False)
+        for m in ["jaccard", "approx_er", "degree"]:
+            if f"backbone_{m}_error" in g:
+                continue
+            _, st = gs.compute_metric_backbone(data, g[f"cost_{m}"], epsilon=1e-9, verbose=False)
+            assert np.array_equal(st["keep_mask"], g[f"backbone_{m}"]), (name, m)
+    ei, n = graphs.rmat(12, 8, seed=2), 1 << 12
+    ip, ix, _ = O.canonical_csr(ei, n)
+    cost = O.scores_to_cost(O.jaccard(ip, ix), "jaccard")
+    assert np.array_equal(backbone_mask(ei, n, cost[: ei.shape[1]]), O.metric_backbone(ei, n, cost))
+    monkeypatch.setenv("GSPARSE_BB_LANDMARKS", "0")
+    for ei, n in [(graphs.rmat(14, 8, seed=3), 1 << 14), _hub_graph()]:
+        ip, ix, _ = O.canonical_csr(ei, n)
+        w = O.scores_to_cost(O.jaccard(ip, ix), "jaccard")[: ei.shape[1]]
+        multi = backbone_mask(ei, n, w)
+        monkeypatch.setenv("GSPARSE_BB_MULTI", "1")
+        single = backbone_mask(ei, n, w)
+        monkeypatch.setenv("GSPARSE_BB_MULTI", S)
+        assert np.array_equal(multi, single)
