@@ -589,12 +589,131 @@ def bench_exact_er(args, world, rank, local_rank, dev, dist):
         dist.destroy_process_group()
 
 
+def bench_scorers(args, world, rank, local_rank, dev, dist):
+    """configs[1] with every scorer: on the Roman-empire stand-in, one step =
+    Jaccard (metrics.py:17-64), Adamic-Adar (:67-121), FeatCos on 300-d float32
+    features (:301-358) and ApproxER (:178-298) over all E edges, inputs
+    resident in HBM.  Per-scorer rooflines by SURVEY 8(d)'s algorithmic bytes
+    (B_J, B_AA, B_F, B_ER); the line's roofline is the dominant kernel's.  CPU
+    baseline: the oracle's NumPy restatements of Jaccard / AA / FeatCos (full)
+    plus the ApproxER sample of the default line.  Replicas at N > 1."""
+    from gsparse import graphs
+    from gsparse._lib import Context
+    from gsparse.engine import Engine, aa_weights, jl_dim
+
+    ei, n, f = graphs.roman_like(), 22_662, 300
+    x = graphs.features(n, f, seed=1)
+    E = ei.shape[1]
+    ctx = Context(local_rank)
+    ctx.set_graph_edge_index(n, torch.from_numpy(np.ascontiguousarray(ei[0])).to(dev),
+                             torch.from_numpy(np.ascontiguousarray(ei[1])).to(dev))
+    eng = Engine(ctx)
+    nnz = eng.nnz
+    k = jl_dim(n, 0.3)
+    indptr, indices, _ = ctx.csr()
+    xd = torch.from_numpy(x).to(dev)
+    cd = torch.from_numpy(np.ascontiguousarray(aa_weights(indptr))).to(dev)
+    outs = [torch.empty(nnz, dtype=torch.float64, device=dev) for _ in range(4)]
+
+    def step():
+        eng.jaccard(0, nnz, out=outs[0])
+        eng.adamic_adar(0, nnz, out=outs[1], c=cd)
+        eng.feature_cosine(xd, 0, nnz, out=outs[2])
+        rng = np.random.default_rng(42)
+        eng.er_prepare(k)
+        eng.er_project_device(rng, k)
+        eng.er_solve(0, k, 500, 1e-6, args.blas_threads)
+        eng.er_scores(0, k, True, out=outs[3])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ctx.profile(True)
+    ctx.profile_reset()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    # SURVEY 8(d) algorithmic bytes (binarised degrees; the graph is symmetric)
+    deg = np.diff(indptr).astype(np.float64)
+    rows = np.repeat(np.arange(n), np.diff(indptr))
+    b_j = 4.0 * float(np.sum(deg[rows] + deg[indices])) + 12.0 * nnz
+    b_aa = b_j + 8.0 * float(np.sum(eng.common_neighbors()))
+    b_f = 2.0 * f * 4 * nnz + 8.0 * nnz + 3.0 * n * f * 4
+
+    def roof(names, by):
+        ms = sum(prof[nm]["ms"] for nm in names if nm in prof)
+        la = max((prof[nm]["launches"] for nm in names if nm in prof), default=0)
+        if not la or ms <= 0:
+            return None
+        avg = ms / la
+        ach = by / (avg * 1e-3) / 1e9
+        return {"kernels": names, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_ms": round(avg, 4),
+                "algorithmic_bytes_per_launch": by}
+
+    per = {"jaccard": roof(["jaccard"], b_j), "adamic_adar": roof(["adamic_adar"], b_aa),
+           "feature_cosine": roof(["featcos_normalise", "featcos_edges"], b_f)}
+    p = prof.get("cg_res") or max(prof.values(), key=lambda v: v["ms"])
+    name = "cg_res" if "cg_res" in prof else max(prof, key=lambda kk: prof[kk]["ms"])
+    avg_ms = p["ms"] / p["launches"]
+    achieved = p["bytes"] / p["launches"] / (avg_ms * 1e-3) / 1e9
+    traffic, tsrc = pmc_traffic(name, "roman") if world == 1 else (None, None)
+    roofline = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": round(traffic) if traffic else None, "avg_launch_ms": round(avg_ms, 5),
+                "algorithmic_bytes_per_launch": p["bytes"] / p["launches"],
+                "launches": p["launches"]}
+    if tsrc:
+        roofline["traffic_source"] = tsrc
+    result = {
+        "metric": "scored edges/sec (Jaccard+AA+FeatCos+ApproxER)",
+        "value": round(world * E * args.steps / elapsed, 1), "unit": "scored edges/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64 (FeatCos in f32, as the reference)",
+        "data": "synthetic (stand-in graph of the config's size; datasets are not downloadable here)",
+        "config": {"workload": "configs[1] Roman-empire all scorers", "n": n, "E": E, "features": f,
+                   "jl_k": k, "cg_maxiter": 500, "blas_threads_order": args.blas_threads,
+                   "parallelism": f"{world} replicas" if world > 1 else "1 GPU"},
+        "roofline": roofline, "scorer_rooflines": per,
+        "kernels": {kk: {"launches": v["launches"], "ms": round(v["ms"], 3)} for kk, v in prof.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import gsparse_oracle as O
+
+        ip, ix, _ = O.canonical_csr(ei, n)
+        t = time.perf_counter()
+        O.adamic_adar(ip, ix)
+        t_aa = time.perf_counter() - t
+        t = time.perf_counter()
+        O.feature_cosine(ip, ix, x)
+        t_fc = time.perf_counter() - t
+        base = cpu_baseline_roman(ei, n, args.cpu_sample_cols, 1)
+        total = base["seconds_extrapolated"] + t_aa + t_fc
+        result["cpu_baseline"] = {
+            "value": float(E / total), "unit": "scored edges/s", "cores": 1, "kind": "port",
+            "sample": f"AA ({t_aa:.2f}s) + FeatCos ({t_fc:.2f}s) in full + " + base["sample"],
+            "seconds_extrapolated": round(total, 3)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="roman", choices=["roman", "rmat", "arxiv", "backbone", "exact_er", "topology", "geodesic"])
+    ap.add_argument("--workload", default="roman", choices=["roman", "rmat", "arxiv", "backbone", "exact_er", "topology", "geodesic", "scorers"])
     ap.add_argument("--scale", type=int, default=22, help="R-MAT scale for --workload rmat")
     ap.add_argument("--bb-graph", default="rmat", choices=["rmat", "roman"],
                     help="graph of --workload backbone (R-MAT at --bb-scale, or Roman-like)")
@@ -638,6 +757,8 @@ def main():
         return bench_topology(args, world, rank, local_rank, dev, dist)
     if args.workload == "geodesic":
         return bench_geodesic(args, world, rank, local_rank, dev, dist)
+    if args.workload == "scorers":
+        return bench_scorers(args, world, rank, local_rank, dev, dist)
 
     t_gen = time.perf_counter()
     if args.workload == "roman":
