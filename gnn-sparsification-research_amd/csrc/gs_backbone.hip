@@ -392,6 +392,31 @@ __global__ void __launch_bounds__(NT) k_bb_sssp(
     if (threadIdx.x == 0) atomicAdd(relax_total, s_relax);
 }
 
+// order-preserving u64 key of a double (0 below every key: "no value")
+__device__ __forceinline__ unsigned long long dkey(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double dkey_val(unsigned long long k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
+}
+
+// S per-source maxima at once: each thread's keys -> wave max -> one LDS atomicMax
+// per wave and source into out[S] (0 on entry); ends with a barrier
+template <int S>
+__device__ __forceinline__ void bb_block_max_s(unsigned long long (&m)[S], unsigned long long *out) {
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+        unsigned long long v = m[k];
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long o = __shfl_xor(v, off, 64);
+            v = o > v ? o : v;
+        }
+        if ((threadIdx.x & 63) == 0 && v) atomicMax(&out[k], v);
+    }
+    __syncthreads();
+}
+
 // S sources per workgroup, searched together: dist[x*S + s] interleaved, so
 // the random read of node x's labels is one 8S-byte segment shared by the S
 // searches (the single-source kernel fetches a whole line per relaxation).
@@ -411,7 +436,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     static_assert(S >= 1 && S <= 8, "1..8 sources per workgroup");
     constexpr int NW = NT / 64;
     __shared__ int s_fcount, s_ncount, s_tcount;
-    __shared__ double s_wmax[S], s_wnext[S];
+    __shared__ double s_wmax[S];
+    __shared__ unsigned long long s_wkey[S];
     __shared__ int64_t s_src[S];
     __shared__ unsigned long long s_relax;
     __shared__ int32_t w_pre[NW][65];
@@ -432,20 +458,30 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
         if (threadIdx.x < S) {
             const int64_t si = bi * S + threadIdx.x;
             s_src[threadIdx.x] = si < nsrc ? sources[si] : -1;
-            s_wmax[threadIdx.x] = -1.0;
+            s_wkey[threadIdx.x] = 0ull;
         }
         __syncthreads();
-        // largest unresolved target weight of each source (-1: nothing to decide)
-        for (int k = 0; k < S; ++k) {
-            double lm = -1.0;
-            const int64_t u = s_src[k];
-            if (u >= 0)
-                for (int64_t j = optr[u] + threadIdx.x; j < optr[u + 1]; j += NT) {
-                    const int64_t idx = order[j];
-                    if (state[idx] == 0 && w[idx] > lm) lm = w[idx];
-                }
-            bb_block_max(lm, &s_wmax[k]);
+        // largest unresolved target weight of each source (none: nothing to decide)
+        {
+            unsigned long long lm[S];
+#pragma unroll
+            for (int k = 0; k < S; ++k) {
+                lm[k] = 0ull;
+                const int64_t u = s_src[k];
+                if (u >= 0)
+                    for (int64_t j = optr[u] + threadIdx.x; j < optr[u + 1]; j += NT) {
+                        const int64_t idx = order[j];
+                        if (state[idx] == 0) {
+                            const unsigned long long kk = dkey(w[idx]);
+                            lm[k] = kk > lm[k] ? kk : lm[k];
+                        }
+                    }
+            }
+            bb_block_max_s<S>(lm, s_wkey);
         }
+        if (threadIdx.x < S)
+            s_wmax[threadIdx.x] = s_wkey[threadIdx.x] ? dkey_val(s_wkey[threadIdx.x]) : -1.0;
+        __syncthreads();
         // seed: every live source at its own node (sources are distinct nodes)
         if (threadIdx.x == 0) {
             int f = 0;
@@ -579,30 +615,36 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                 }
             }
             // hook: prune targets per source, lower its bound, end when all are done
-            if (threadIdx.x < S) s_wnext[threadIdx.x] = -1.0;
+            if (threadIdx.x < S) s_wkey[threadIdx.x] = 0ull;
             __syncthreads();
-            for (int k = 0; k < S; ++k) {
-                double mx = -1.0;
-                const int64_t u = s_src[k];
-                if (u >= 0 && s_wmax[k] >= 0.0)
-                    for (int64_t j = optr[u] + threadIdx.x; j < optr[u + 1]; j += NT) {
-                        const int64_t idx = order[j];
-                        if (state[idx] != 0) continue;
-                        const unsigned long long db = __hip_atomic_load(
-                            &dist[dst[idx] * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (db != kInfBits && w[idx] > __longlong_as_double((long long)db) + eps) {
-                            state[idx] = 2;
-                            continue;
+            {
+                unsigned long long mx[S];
+#pragma unroll
+                for (int k = 0; k < S; ++k) {
+                    mx[k] = 0ull;
+                    const int64_t u = s_src[k];
+                    if (u >= 0 && s_wmax[k] >= 0.0)
+                        for (int64_t j = optr[u] + threadIdx.x; j < optr[u + 1]; j += NT) {
+                            const int64_t idx = order[j];
+                            if (state[idx] != 0) continue;
+                            const unsigned long long db = __hip_atomic_load(
+                                &dist[dst[idx] * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (db != kInfBits &&
+                                w[idx] > __longlong_as_double((long long)db) + eps) {
+                                state[idx] = 2;
+                                continue;
+                            }
+                            const unsigned long long kk = dkey(w[idx]);
+                            mx[k] = kk > mx[k] ? kk : mx[k];
                         }
-                        mx = w[idx] > mx ? w[idx] : mx;
-                    }
-                bb_block_max(mx, &s_wnext[k]);
+                }
+                bb_block_max_s<S>(mx, s_wkey);
             }
             if (threadIdx.x == 0) {
                 bool any = false;
                 for (int k = 0; k < S; ++k) {
-                    s_wmax[k] = s_wnext[k];
-                    any = any || s_wnext[k] >= 0.0;
+                    s_wmax[k] = s_wkey[k] ? dkey_val(s_wkey[k]) : -1.0;
+                    any = any || s_wkey[k] != 0ull;
                 }
                 if (!any) s_fcount = 0;
             }
