@@ -1385,27 +1385,36 @@ __global__ void __launch_bounds__(kResThreads) k_cg_resident(ResArgs A, ChunkArg
             if (it == 0) {
                 for (int64_t i = tid; i < n; i += kResThreads) p[i] = r[i];
             } else {
-                // 8 rows per thread in flight (Roman: 82.6 vs 86.8 ms of workgroup 0's
-                // 465 / 470 ms with 4)
-                constexpr int U = 8;
-                for (int64_t i0 = tid; i0 < n; i0 += kResThreads * U) {
-                    double po[U], rv[U], xv[U];
+                // 8 rows per thread in flight as 4 row pairs (16-B loads; the odd row n of
+                // an odd n is slot padding, written but never read)
+                constexpr int U = 4;
+                const int64_t n2 = (n + 1) >> 1;
+                double2 *p2 = reinterpret_cast<double2 *>(p);
+                const double2 *r2 = reinterpret_cast<const double2 *>(r);
+                double2 *x2 = reinterpret_cast<double2 *>(x);
+                for (int64_t j0 = tid; j0 < n2; j0 += kResThreads * U) {
+                    double2 po[U], rv[U], xv[U];
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
-                        const int64_t i = i0 + (int64_t)u * kResThreads;
-                        const int64_t ic = i < n ? i : i0;
-                        po[u] = p[ic];
-                        rv[u] = r[ic];
-                        xv[u] = it > 1 ? x[ic] : 0.0;
+                        const int64_t j = j0 + (int64_t)u * kResThreads;
+                        const int64_t jc = j < n2 ? j : j0;
+                        po[u] = p2[jc];
+                        rv[u] = r2[jc];
+                        xv[u] = it > 1 ? x2[jc] : make_double2(0.0, 0.0);
                     }
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
-                        const int64_t i = i0 + (int64_t)u * kResThreads;
-                        if (i < n) {
-                            const double t1 = alpha_prev * po[u];
-                            x[i] = xv[u] + t1;
-                            const double pb = po[u] * beta;
-                            p[i] = pb + rv[u];
+                        const int64_t j = j0 + (int64_t)u * kResThreads;
+                        if (j < n2) {
+                            double2 xo, pn;
+                            const double t1a = alpha_prev * po[u].x, t1b = alpha_prev * po[u].y;
+                            xo.x = xv[u].x + t1a;
+                            xo.y = xv[u].y + t1b;
+                            const double pba = po[u].x * beta, pbb = po[u].y * beta;
+                            pn.x = pba + rv[u].x;
+                            pn.y = pbb + rv[u].y;
+                            x2[j] = xo;
+                            p2[j] = pn;
                         }
                     }
                 }
