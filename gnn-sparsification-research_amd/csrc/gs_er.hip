@@ -1152,6 +1152,7 @@ struct ResArgs {
     int64_t ql;              // rows of q mirrored in LDS (dynamic shared memory)
     int64_t nstab;           // SELL slices whose (offset, width) are staged in LDS after q (0: none)
     long long *prof;         // optional: workgroup 0's phase times (wall clock ticks)
+    int32_t dcount;          // unit form: every L_reg_ii == fl((entries of row i) - 1 + 1e-6)
 };
 
 // a wave-uniform copy of v (read from lane 0): loop and branch conditions that
@@ -1196,7 +1197,9 @@ __device__ __forceinline__ void res_spmv(const ResArgs &A, const double *p, doub
             }
             w[i] = ok[i] ? wb : 0;
             wmax = w[i] > wmax ? w[i] : wmax;
-            dg[i] = UNIT ? A.sdiag[row[i]] : 0.0;
+            // the diagonal: derived from the row's entry count when the whole row is in
+            // the first W entries (dcount graphs), else loaded
+            dg[i] = (UNIT && !(A.dcount && w[i] <= W)) ? A.sdiag[row[i]] : 0.0;
             acc[i] = 0.0;
         }
         {
@@ -1210,6 +1213,16 @@ __device__ __forceinline__ void res_spmv(const ResArgs &A, const double *p, doub
                     col[i][k] = A.scol[idx];
                     if (!UNIT) v[i][k] = A.sval[idx];
                 }
+            if (UNIT && A.dcount) {
+#pragma unroll
+                for (int i = 0; i < RB; ++i)
+                    if (w[i] <= W) {
+                        int cnt = 0;
+#pragma unroll
+                        for (int k = 0; k < W; ++k) cnt += (k < w[i] && col[i][k] >= 0) ? 1 : 0;
+                        dg[i] = (double)(cnt - 1) + 1e-6;
+                    }
+            }
 #pragma unroll
             for (int i = 0; i < RB; ++i)
 #pragma unroll
@@ -1503,7 +1516,8 @@ __global__ void k_l_unit(const int64_t *__restrict__ lp, const int32_t *__restri
             else unit = unit && lv[e] == -1.0;
         }
         diag[i] = dg;
-        if (!unit) *flag = 0;
+        if (!unit) atomicAnd(flag, ~1);
+        if (!(dg == (double)(lp[i + 1] - lp[i] - 1) + 1e-6)) atomicAnd(flag, ~2);
     }
 }
 
@@ -1804,7 +1818,7 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             // unit-weight test + diagonal, then the SELL-16 copy of L_reg
             auto *sdiag = (double *)c->buf("er_sell_diag").ensure(sizeof(double) * (n + 1));
             auto *uflag = (int32_t *)c->buf("er_unit_flag").ensure(sizeof(int32_t));
-            int32_t one = 1, unit = 0;
+            int32_t one = 3, unit = 0;  // bit 0: unit weights, bit 1: diagonal = entries - 1 + 1e-6
             GS_HIP(hipMemcpyAsync(uflag, &one, sizeof(one), hipMemcpyHostToDevice, c->stream));
             if (n)
                 k_l_unit<<<grid_for(n, 256, 8192), 256, 0, c->stream>>>(lp, li, lv, n, sdiag, uflag);
@@ -1819,6 +1833,8 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             GS_HIP(hipMemcpyAsync(&sent, soff + nbk, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
             GS_HIP(hipMemcpyAsync(&unit, uflag, sizeof(unit), hipMemcpyDeviceToHost, c->stream));
             GS_HIP(hipStreamSynchronize(c->stream));
+            const int32_t dcount = (unit & 3) == 3 ? 1 : 0;
+            unit &= 1;
             if (const char *e = getenv("GSPARSE_RES_UNIT")) unit = unit && atoi(e) != 0;
             // longest row (the SELL block widths hold it) -> ELL width 4 / 8 / 12 / 16, else SELL
             int32_t maxw = 0;
@@ -1854,7 +1870,9 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             if (getenv("GSPARSE_RES_PROF"))
                 rprof = (long long *)c->buf("er_res_prof").ensure(8 * sizeof(long long));
             ResArgs ra{n, er.ld, ldn, col0, ncols, lp, li, lv, Rr, Xc, sl, ca, cl, maxiter, rtol,
-                       cp.iters, soff, swid, scol, sval, sdiag, ecol, evalp, lde, 0, 0, rprof};
+                       cp.iters, soff, swid, scol, sval, sdiag, ecol, evalp, lde, 0, 0, rprof,
+                       dcount};
+            if (const char *e = getenv("GSPARSE_RES_DCOUNT")) ra.dcount = ra.dcount && atoi(e) != 0;
             // q mirror in LDS: what the 160 KiB leave after the static 16 KiB
             // dynamic LDS (140 KiB next to the 16 KiB chain table): the SELL slice table
             // (8 B per 16 rows, when the offsets fit int32) and a mirror of q's first rows
