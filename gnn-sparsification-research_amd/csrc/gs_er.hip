@@ -1813,6 +1813,12 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             int64_t slots = 256;
             if (const char *e = getenv("GSPARSE_CG_SLOTS")) slots = atoi(e) > 0 ? atoi(e) : slots;
             if (slots > ncols) slots = ncols;
+            // as few workgroups as the round count allows (every workgroup then owns the
+            // same number of columns, and fewer CUs share the Infinity Cache in each round)
+            if (slots > 0 && !getenv("GSPARSE_CG_SLOTS")) {
+                const int64_t rounds = (ncols + slots - 1) / slots;
+                slots = (ncols + rounds - 1) / rounds;
+            }
             double *Xc = (double *)c->buf("er_xc").ensure(sizeof(double) * (size_t)ncols * ldn);
             double *sl = (double *)c->buf("er_slots").ensure(sizeof(double) * (size_t)slots * 3 * ldn);
             // unit-weight test + diagonal, then the SELL-16 copy of L_reg
