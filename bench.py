@@ -89,6 +89,27 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_info():
+    """CPU model and logical CPU count of the box (state the cores)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "logical_cpus": os.cpu_count()}
+
+
+def emit(result):
+    """The one JSON line; the CPU baseline names the host it ran on."""
+    if isinstance(result.get("cpu_baseline"), dict):
+        result["cpu_baseline"]["host"] = host_info()
+    print(json.dumps(result), flush=True)
+
+
 def cpu_baseline_roman(ei, n, sample_cols, threads):
     """The reference algorithm restated with identical NumPy/SciPy calls
     (oracle/gsparse_oracle.py), timed on a bounded sample of the same
@@ -296,7 +317,7 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_backbone(ei, n, cost)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
     if dist:
         dist.destroy_process_group()
 
@@ -407,7 +428,7 @@ def bench_topology(args, world, rank, local_rank, dev, dist):
                                             "connected_components, algebraic_connectivity "
                                             f"tracemin_lu), one full call: {sec:.2f} s"}
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
 
 
 def bench_geodesic(args, world, rank, local_rank, dev, dist):
@@ -484,7 +505,7 @@ def bench_geodesic(args, world, rank, local_rank, dev, dist):
                                   "sample": "the reference's NetworkX calls (shortest_path_length "
                                             f"hop + Dijkstra, 500 pairs each), one full step: {sec:.2f} s"}
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
 
 
 def bench_exact_er(args, world, rank, local_rank, dev, dist):
@@ -584,7 +605,7 @@ def bench_exact_er(args, world, rank, local_rank, dev, dist):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_exact_er(a.indptr, a.indices, a.data, n)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
     if dist:
         dist.destroy_process_group()
 
@@ -705,7 +726,7 @@ def bench_scorers(args, world, rank, local_rank, dev, dist):
             "sample": f"AA ({t_aa:.2f}s) + FeatCos ({t_fc:.2f}s) in full + " + base["sample"],
             "seconds_extrapolated": round(total, 3)}
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
 
 
 def main():
@@ -880,7 +901,7 @@ def main():
         elif args.workload == "rmat":
             result["cpu_baseline"] = cpu_baseline_jaccard(ei, n, 1)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
     if dist:
         dist.destroy_process_group()
 
