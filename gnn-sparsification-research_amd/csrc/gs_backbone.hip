@@ -205,7 +205,7 @@ __device__ void bb_search(const int64_t *__restrict__ gp, const int32_t *__restr
                 b = gp[x];
                 deg = (int)(gp[x + 1] - b);
                 dx = __longlong_as_double(
-                    (long long)__hip_atomic_load(&dist[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    (long long)__hip_atomic_load(&dist[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
             }
             int incl = deg;
             for (int off = 1; off < 64; off <<= 1) {
@@ -246,7 +246,7 @@ __device__ void bb_search(const int64_t *__restrict__ gp, const int32_t *__restr
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     cur_d[u] = go[u] ? __hip_atomic_load(&dist[y[u]], __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP)
                                      : 0ull;
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -351,7 +351,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp(
                 const int64_t idx = order[j];
                 if (state[idx] != 0) continue;
                 const unsigned long long db =
-                    __hip_atomic_load(&dist[dst[idx]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_load(&dist[dst[idx]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (db != kInfBits && w[idx] > __longlong_as_double((long long)db) + eps) {
                     state[idx] = 2;
                     continue;
@@ -373,7 +373,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp(
             if (state[idx] != 0) continue;
             int64_t v = dst[idx];
             unsigned long long db =
-                __hip_atomic_load(&dist[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_load(&dist[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             double d = __longlong_as_double((long long)db);
             bool keep = (db == kInfBits) || (w[idx] <= d + eps);
             state[idx] = keep ? 1 : 2;
@@ -522,7 +522,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
 #pragma unroll
                     for (int k = 0; k < S; ++k)
                         w_d[wv][lane][k] = __longlong_as_double((long long)__hip_atomic_load(
-                            &dist[(int64_t)x * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                            &dist[(int64_t)x * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
                 }
                 int incl = deg;
                 for (int off = 1; off < 64; off <<= 1) {
@@ -566,7 +566,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                         for (int k = 0; k < S; ++k)
                             cd[u][k] = ((mm[u] >> k) & 1u)
                                            ? __hip_atomic_load(&dist[(int64_t)y[u] * S + k],
-                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
                                            : 0ull;
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
@@ -628,7 +628,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                             const int64_t idx = order[j];
                             if (state[idx] != 0) continue;
                             const unsigned long long db = __hip_atomic_load(
-                                &dist[dst[idx] * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                &dist[dst[idx] * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             if (db != kInfBits &&
                                 w[idx] > __longlong_as_double((long long)db) + eps) {
                                 state[idx] = 2;
@@ -658,7 +658,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                 const int64_t idx = order[j];
                 if (state[idx] != 0) continue;
                 const unsigned long long db = __hip_atomic_load(
-                    &dist[dst[idx] * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    &dist[dst[idx] * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const double d = __longlong_as_double((long long)db);
                 state[idx] = ((db == kInfBits) || (w[idx] <= d + eps)) ? 1 : 2;
             }
