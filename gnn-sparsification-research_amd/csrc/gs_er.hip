@@ -1844,11 +1844,25 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             if (const char *e = getenv("GSPARSE_RES_UNIT")) unit = unit && atoi(e) != 0;
             // longest row (the SELL block widths hold it) -> ELL width 4 / 8 / 12 / 16, else SELL
             int32_t maxw = 0;
+            int sell_w = 8;
             {
                 std::vector<int32_t> hw((size_t)nbk);
                 if (nbk)
                     GS_HIP(hipMemcpy(hw.data(), swid, sizeof(int32_t) * nbk, hipMemcpyDeviceToHost));
                 for (int32_t v : hw) maxw = v > maxw ? v : maxw;
+                // entries per row loaded at once: the smallest W in 6..8 that leaves at most
+                // 1 in 10 of the 64-row tiles (a wave's rows, 4 slices) to the tail loop
+                const int64_t ntl = (nbk + 3) / 4;
+                for (int wc = 6; wc <= 8; ++wc) {
+                    int64_t over = 0;
+                    for (int64_t t = 0; t < ntl; ++t) {
+                        int32_t m = 0;
+                        for (int64_t b = 4 * t; b < 4 * t + 4 && b < nbk; ++b) m = hw[b] > m ? hw[b] : m;
+                        over += m > wc;
+                    }
+                    sell_w = wc;
+                    if (over * 10 <= ntl) break;
+                }
             }
             // (measured on the Roman layout: SELL-16 40 us per column-iteration vs ELL-12 48 us --
             // the padded index loads cost more than the dependent block-offset load saves)
@@ -1897,14 +1911,19 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));     \
         k_cg_resident<B, W, C, U, E><<<(unsigned)slots, kResThreads, dyn, c->stream>>>(ra, ch); \
     } while (0)
-            // SpMV rows per thread-trip and entries loaded at once: 2 x 8 (Roman: 36 us per
-            // column-iteration vs 40 us for 4 x 4, whose rows wider than 4 take the tail loop)
-            int rbw = 28;
-            if (const char *e = getenv("GSPARSE_RES_RBW")) rbw = atoi(e) == 44 ? 44 : 28;
+            // SpMV rows per thread-trip and entries loaded at once: 2 x W, W from the slice
+            // widths above (Roman: W = 7, 419 ms per step vs 439 with 8 and 427 with 6;
+            // 4 x 4 was slower, its rows wider than 4 take the tail loop)
+            int rbw = 20 + sell_w;
+            if (const char *e = getenv("GSPARSE_RES_RBW")) rbw = atoi(e) == 44 ? 44 : atoi(e) == 27 ? 27 : atoi(e) == 26 ? 26 : 28;
 #define GS_RES_U(E)                                                  \
     do {                                                             \
         if (rbw == 28) {                                             \
             if (unit) GS_RES(2, 8, 16, true, E); else GS_RES(2, 8, 16, false, E); \
+        } else if (rbw == 27) {                                      \
+            if (unit) GS_RES(2, 7, 16, true, E); else GS_RES(2, 7, 16, false, E); \
+        } else if (rbw == 26) {                                      \
+            if (unit) GS_RES(2, 6, 16, true, E); else GS_RES(2, 6, 16, false, E); \
         } else {                                                     \
             if (unit) GS_RES(4, 4, 16, true, E); else GS_RES(4, 4, 16, false, E); \
         }                                                            \

@@ -108,10 +108,12 @@ def chunked_er():
                                  {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_RBW": "44"},
                                  {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_RBW": "44",
                                   "GSPARSE_RES_UNIT": "0"},
-                                 {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_DCOUNT": "0"}],
+                                 {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_DCOUNT": "0"},
+                                 {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_RBW": "26"},
+                                 {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_RBW": "28"}],
                          ids=["m0", "m1", "m3", "m4", "m4-ell", "m4-q-global", "m4-7slots",
                               "m4-weighted-sell", "m4-weighted-ell", "m4-slices-global",
-                              "m4-rb4w4", "m4-rb4w4-weighted", "m4-diag-loaded"])
+                              "m4-rb4w4", "m4-rb4w4-weighted", "m4-diag-loaded", "m4-w6", "m4-w8"])
 @pytest.mark.parametrize("threads", [3, 8])
 @pytest.mark.parametrize("graph", ["unit", "dup", "hub"])
 def test_approx_er_blas_chunks_vs_oracle(gs, chunked_er, graph, threads, env, monkeypatch):
