@@ -183,6 +183,10 @@ void gs_destroy(gs_ctx *c) {
     c->outbuf.release();
     c->inbuf.release();
     c->inbuf2.release();
+    for (auto &a : c->aux)
+        if (a) (void)hipStreamDestroy(a);
+    for (auto &e : c->aux_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }

@@ -113,6 +113,8 @@ struct gs_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
+    hipStream_t aux[4] = {nullptr, nullptr, nullptr, nullptr};  // side streams (Jaccard classes)
+    hipEvent_t aux_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     bool async_ = false;
     bool profiling = false;
     std::map<std::string, gs::ProfEntry> prof;

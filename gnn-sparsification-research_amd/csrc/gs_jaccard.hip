@@ -434,10 +434,27 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts)
     GS_HIP(hipStreamSynchronize(st));  // the only sync unless bitmap rows exist
     int64_t tmax = 1;
     for (int k = 0; k < kJacClasses; ++k) tmax = (int64_t)htot[k] > tmax ? (int64_t)htot[k] : tmax;
-    // task lists are reused class after class (stream order): size them once
-    auto *trow = (int32_t *)c->buf("jac_trow").ensure(sizeof(int32_t) * tmax);
-    auto *ti = (int32_t *)c->buf("jac_ti").ensure(sizeof(int32_t) * tmax);
+    // the hash classes run concurrently on side streams (a class of big LDS tables
+    // fills one or two workgroups per CU; the others use the rest): each gets its own
+    // task lists; the bitmap class stays on the context stream
+    (void)tmax;
+    bool conc = true;
+    if (const char *e = getenv("GSPARSE_JAC_CONCURRENT")) conc = atoi(e) != 0;
+    if (conc) {
+        for (auto &a : c->aux)
+            if (!a) GS_HIP(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
+        for (auto &e : c->aux_ev)
+            if (!e) GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    int launched = 0;
     for (int k = 0; k < kJacClasses; ++k) {
+        static const char *const kTrow[kJacClasses] = {"jac_trow0", "jac_trow1", "jac_trow2",
+                                                      "jac_trow3", "jac_trow4"};
+        static const char *const kTi[kJacClasses] = {"jac_ti0", "jac_ti1", "jac_ti2", "jac_ti3",
+                                                    "jac_ti4"};
+        const int64_t sz = htot[k] ? (int64_t)htot[k] : 1;
+        auto *trow = (int32_t *)c->buf(conc ? kTrow[k] : "jac_trow").ensure(sizeof(int32_t) * (conc ? sz : tmax));
+        auto *ti = (int32_t *)c->buf(conc ? kTi[k] : "jac_ti").ensure(sizeof(int32_t) * (conc ? sz : tmax));
         const bool giant = k == kJacBitmap;
         const int64_t ntot = (int64_t)htot[k], ngiant = giant ? (int64_t)htot[kJacClasses] : 0;
         if (!ntot) continue;
@@ -458,14 +475,22 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts)
         const int64_t tlo = share(ntot, part), thi = share(ntot, part + 1);
         const unsigned nb = (unsigned)(thi - tlo);
         if (k < kJacBitmap && !nb) continue;
+        // hash classes: on side stream k once the task lists are emitted
+        hipStream_t hs = st;
+        if (conc && k < kJacBitmap) {
+            GS_HIP(hipEventRecord(c->aux_ev[k], st));
+            GS_HIP(hipStreamWaitEvent(c->aux[k], c->aux_ev[k], 0));
+            hs = c->aux[k];
+            launched |= 1 << k;
+        }
         if (k == 0) {
-            k_jac_hash<2048><<<nb, 256, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
+            k_jac_hash<2048><<<nb, 256, 0, hs>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
         } else if (k == 1) {
-            k_jac_hash<8192><<<nb, 512, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
+            k_jac_hash<8192><<<nb, 512, 0, hs>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
         } else if (k == 2) {
-            k_jac_hash<16384><<<nb, 1024, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
+            k_jac_hash<16384><<<nb, 1024, 0, hs>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
         } else if (k == 3) {
-            k_jac_hash<32768><<<nb, 1024, 0, st>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
+            k_jac_hash<32768><<<nb, 1024, 0, hs>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
         } else {
             // bitmaps in batches of rows (<= 1 GiB of bits at a time)
             const int64_t words = (n + 31) / 32;
@@ -500,6 +525,12 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts)
         }
         GS_HIP(hipGetLastError());
     }
+    // join the side streams back into the context stream
+    for (int k = 0; k < kJacBitmap; ++k)
+        if (launched & (1 << k)) {
+            GS_HIP(hipEventRecord(c->aux_ev[k], c->aux[k]));
+            GS_HIP(hipStreamWaitEvent(st, c->aux_ev[k], 0));
+        }
     prof_end(c, t0, counts ? "common_neighbors" : "jaccard", algo);
 }
 
