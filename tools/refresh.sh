@@ -26,6 +26,6 @@ fi
 if [ -n "${WITH_EXTRA:-}" ]; then
   timeout -k 10 400 python bench.py --workload scorers > "$O/scorers_bench.json" 2> "$O/scorers_bench.err" || { tail -5 "$O/scorers_bench.err"; exit 1; }
   timeout -k 10 300 python bench.py --workload arxiv --no-cpu-baseline > "$O/arxiv_bench.json" 2> "$O/arxiv_bench.err" || { tail -5 "$O/arxiv_bench.err"; exit 1; }
-  timeout -k 10 300 python bench.py --workload rmat > "$O/rmat_bench.json" 2> "$O/rmat_bench.err" || { tail -5 "$O/rmat_bench.err"; exit 1; }
+  timeout -k 10 300 python bench.py --workload rmat --no-cpu-baseline > "$O/rmat_bench.json" 2> "$O/rmat_bench.err" || { tail -5 "$O/rmat_bench.err"; exit 1; }
   echo extra done
 fi
