@@ -1400,7 +1400,7 @@ __global__ void __launch_bounds__(kResThreads) k_cg_resident(ResArgs A, ChunkArg
             } else {
                 // 8 rows per thread in flight as 4 row pairs (16-B loads; the odd row n of
                 // an odd n is slot padding, written but never read)
-                constexpr int U = 4;
+                constexpr int U = 6;
                 const int64_t n2 = (n + 1) >> 1;
                 double2 *p2 = reinterpret_cast<double2 *>(p);
                 const double2 *r2 = reinterpret_cast<const double2 *>(r);
