@@ -1,0 +1,34 @@
+"""T_api: the drop-in API's wall time with host NumPy in and out --
+GraphSparsifier(data) (CSR build), compute_scores("jaccard") and
+compute_scores("approx_er") on the Roman-like graph, PCIe transfers included."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "gnn-sparsification-research_amd"))
+import gsparse  # noqa: E402
+from gsparse import graphs  # noqa: E402
+
+ei, n = graphs.roman_like(), 22_662
+data = gsparse.Data(edge_index=torch.from_numpy(ei), num_nodes=n)
+out = {}
+for rep in range(2):  # the first pass includes context creation and code loading
+    t = time.perf_counter()
+    sp = gsparse.GraphSparsifier(data, "cuda:0")
+    t_init = time.perf_counter() - t
+    t = time.perf_counter()
+    jac = sp.compute_scores("jaccard")
+    t_jac = time.perf_counter() - t
+    t = time.perf_counter()
+    er = sp.compute_scores("approx_er")
+    t_er = time.perf_counter() - t
+    out = {"init_s": round(t_init, 4), "jaccard_s": round(t_jac, 4), "approx_er_s": round(t_er, 4),
+           "total_s": round(t_init + t_jac + t_er, 4),
+           "scored_edges_per_s": round(ei.shape[1] / (t_init + t_jac + t_er), 1),
+           "checksum": [float(np.sum(jac)), float(np.sum(er))]}
+print(json.dumps(out))
