@@ -680,7 +680,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
 
 // Full searches from K landmarks: D[x*K + l] = d_fl(landmark l, x) (+inf if
 // unreachable).  One workgroup per landmark.
-__global__ void __launch_bounds__(256) k_bb_landmarks(
+__global__ void __launch_bounds__(1024) k_bb_landmarks(
     const int64_t *__restrict__ gp, const int32_t *__restrict__ gi, const double *__restrict__ gw,
     int64_t n, const int32_t *__restrict__ lm, int K, int max_rounds, double *__restrict__ D,
     int32_t *__restrict__ complete, unsigned long long *__restrict__ dist_all,
@@ -1086,8 +1086,11 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                                                                                    kInfBits);
                 GS_HIP(hipMemsetAsync(lq, 0, 4 * (size_t)K * n, s));
                 int32_t *lcomp = (int32_t *)b_lcomp.ensure(4 * K);
-                k_bb_landmarks<<<(unsigned)K, 256, 0, s>>>(gp, gi, gw, n, dlm, K, kBbLandmarkRounds, D,
-                                                           lcomp, ldist, lq, lfr, ltouch);
+                // one workgroup per landmark: 1,024 threads on large graphs (the K searches
+                // are the only work in flight then)
+                const unsigned lt = n > 65536 ? 1024 : 256;
+                k_bb_landmarks<<<(unsigned)K, lt, 0, s>>>(gp, gi, gw, n, dlm, K, kBbLandmarkRounds, D,
+                                                          lcomp, ldist, lq, lfr, ltouch);
                 const double mrg = std::max(1e-8, 8.0 * (double)n * 0x1p-53);
                 k_bb_certify<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, dw, E, gp, gi, gw, D,
                                                                    lcomp, K, eps, mrg, state);
