@@ -969,11 +969,15 @@ static void bb_build_graph(gs_ctx *c, int64_t n, int64_t E, const int64_t *dsrc,
 }
 
 extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const int64_t *src,
-                                       const int64_t *dst, const double *w, int loc, double eps,
-                                       int part, int nparts, uint8_t *keep, int keep_loc,
-                                       int64_t *n_relax) {
+                                       const int64_t *dst, const double *w, int64_t nw, int loc,
+                                       double eps, int part, int nparts, uint8_t *keep,
+                                       int keep_loc, int64_t *n_relax) {
     return guard([&] {
         GS_CHECK(c, GS_EINVAL, "null context");
+        // the reference indexes edge_weights[idx] for every column (metric_backbone.py:73-74)
+        GS_CHECK(nw >= E, GS_EINDEX, "index %lld is out of bounds for axis 0 with size %lld",
+                 (long long)nw, (long long)nw);
+        GS_CHECK(E == 0 || (src && dst && w && keep), GS_EINVAL, "null column/weight/keep array");
         GS_CHECK(nparts >= 1 && 0 <= part && part < nparts, GS_EINVAL, "bad part %d of %d", part,
                  nparts);
         GS_CHECK(n >= 0 && E >= 0, GS_EINVAL, "negative n/E");
@@ -1062,12 +1066,14 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
             int K = 16;
             if (const char *e = getenv("GSPARSE_BB_LANDMARKS")) K = atoi(e) < 0 ? 0 : atoi(e);
             if (K > n) K = (int)n;
+            // landmark ids: host source of an async copy, alive until the stream sync below
+            std::vector<int32_t> ids;
             if (K > 0) {
                 // landmarks: the K highest-degree nodes of G
                 std::vector<int64_t> hgp(n + 1);
                 GS_HIP(hipMemcpyAsync(hgp.data(), gp, 8 * (n + 1), hipMemcpyDeviceToHost, s));
                 GS_HIP(hipStreamSynchronize(s));
-                std::vector<int32_t> ids(n);
+                ids.resize(n);
                 for (int64_t x = 0; x < n; ++x) ids[x] = (int32_t)x;
                 std::partial_sort(ids.begin(), ids.begin() + K, ids.end(), [&](int32_t p, int32_t q) {
                     const int64_t dp = hgp[p + 1] - hgp[p], dq = hgp[q + 1] - hgp[q];
@@ -1187,16 +1193,19 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
 }
 
 extern "C" int gs_metric_backbone(gs_ctx *c, int64_t n, int64_t E, const int64_t *src,
-                                  const int64_t *dst, const double *w, int loc, double eps,
-                                  uint8_t *keep, int keep_loc, int64_t *n_relax) {
-    return gs_metric_backbone_part(c, n, E, src, dst, w, loc, eps, 0, 1, keep, keep_loc, n_relax);
+                                  const int64_t *dst, const double *w, int64_t nw, int loc,
+                                  double eps, uint8_t *keep, int keep_loc, int64_t *n_relax) {
+    return gs_metric_backbone_part(c, n, E, src, dst, w, nw, loc, eps, 0, 1, keep, keep_loc,
+                                   n_relax);
 }
 
 extern "C" int gs_pair_distances(gs_ctx *c, int64_t n, int64_t E, const int64_t *src,
-                                 const int64_t *dst, const double *w, int loc, int64_t nq,
-                                 const int64_t *qs, const int64_t *qt, double *out) {
+                                 const int64_t *dst, const double *w, int64_t nw, int loc,
+                                 int64_t nq, const int64_t *qs, const int64_t *qt, double *out) {
     return guard([&] {
         GS_CHECK(c, GS_EINVAL, "null context");
+        GS_CHECK(!w || nw >= E, GS_EINDEX, "index %lld is out of bounds for axis 0 with size %lld",
+                 (long long)nw, (long long)nw);
         GS_CHECK(n >= 0 && E >= 0 && nq >= 0, GS_EINVAL, "negative n/E/nq");
         GS_CHECK(n < (int64_t(1) << 31), GS_EUNSUPPORTED, "n >= 2^31");
         GS_CHECK(nq == 0 || (qs && qt && out), GS_EINVAL, "null query arrays");

@@ -187,6 +187,7 @@ void gs_destroy(gs_ctx *c) {
         if (a) (void)hipStreamDestroy(a);
     for (auto &e : c->aux_ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -196,6 +197,30 @@ int gs_set_stream(gs_ctx *c, void *s) {
         GS_CHECK(c, GS_EINVAL, "null context");
         GS_HIP(hipSetDevice(c->device));
         c->stream = s ? (hipStream_t)s : c->own_stream;
+    });
+}
+
+// Cross-stream ordering with a caller's stream (e.g. torch's current stream):
+// an event recorded on the producer, waited on by the consumer -- no host sync.
+static void order_streams(gs_ctx *c, hipStream_t producer, hipStream_t consumer) {
+    GS_HIP(hipSetDevice(c->device));
+    if (producer == consumer) return;
+    if (!c->order_ev) GS_HIP(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
+    GS_HIP(hipEventRecord(c->order_ev, producer));
+    GS_HIP(hipStreamWaitEvent(consumer, c->order_ev, 0));
+}
+
+int gs_stream_wait(gs_ctx *c, void *s) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        order_streams(c, (hipStream_t)s, c->stream);
+    });
+}
+
+int gs_stream_signal(gs_ctx *c, void *s) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        order_streams(c, c->stream, (hipStream_t)s);
     });
 }
 

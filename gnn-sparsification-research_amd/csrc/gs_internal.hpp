@@ -115,6 +115,7 @@ struct gs_ctx {
     hipStream_t stream = nullptr;
     hipStream_t aux[4] = {nullptr, nullptr, nullptr, nullptr};  // side streams (Jaccard classes)
     hipEvent_t aux_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t order_ev = nullptr;  // gs_stream_wait / gs_stream_signal (timing off)
     bool async_ = false;
     bool profiling = false;
     std::map<std::string, gs::ProfEntry> prof;

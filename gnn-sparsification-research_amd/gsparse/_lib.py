@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPARSE_LIB", os.path.join(_HERE, "libgsparse.so"))
 
 GS_HOST, GS_DEVICE = 0, 1
-GS_OK, GS_EINVAL, GS_EHIP, GS_ENOMEM, GS_ESTATE, GS_EUNSUPPORTED = 0, -1, -2, -3, -4, -5
+GS_OK, GS_EINVAL, GS_EHIP, GS_ENOMEM, GS_ESTATE, GS_EUNSUPPORTED, GS_EINDEX = 0, -1, -2, -3, -4, -5, -6
 
 _i64 = ctypes.c_int64
 _i32 = ctypes.c_int32
@@ -33,6 +33,8 @@ SIGNATURES = {
     "gs_create": (_int, [_int, ctypes.POINTER(_vp)]),
     "gs_destroy": (None, [_vp]),
     "gs_set_stream": (_int, [_vp, _vp]),
+    "gs_stream_wait": (_int, [_vp, _vp]),
+    "gs_stream_signal": (_int, [_vp, _vp]),
     "gs_synchronize": (_int, [_vp]),
     "gs_set_async": (_int, [_vp, _int]),
     "gs_profile_enable": (_int, [_vp, _int]),
@@ -60,17 +62,24 @@ SIGNATURES = {
     "gs_topk_mask": (_int, [_vp, _vp, _int, _i64, _i64, _i64, _int, _vp, _int,
                             ctypes.POINTER(_f64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "gs_segment_argmax": (_int, [_vp, _vp, _int, _i64, _vp, _int, _i64, _i64, _vp, _int]),
-    "gs_metric_backbone": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _int, _f64, _vp, _int,
+    "gs_metric_backbone": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _i64, _int, _f64, _vp, _int,
                                   ctypes.POINTER(_i64)]),
-    "gs_metric_backbone_part": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _int, _f64, _int, _int,
-                                       _vp, _int, ctypes.POINTER(_i64)]),
+    "gs_metric_backbone_part": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _i64, _int, _f64, _int,
+                                       _int, _vp, _int, ctypes.POINTER(_i64)]),
     "gs_exact_er": (_int, [_vp, _vp, _int, ctypes.POINTER(_i32)]),
-    "gs_pair_distances": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _int, _i64, _vp, _vp, _vp]),
+    "gs_pair_distances": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _i64, _int, _i64, _vp, _vp,
+                                 _vp]),
     "gs_common_neighbors": (_int, [_vp, _vp, _int]),
     "gs_clustering": (_int, [_vp, ctypes.POINTER(_f64), _vp, _int]),
     "gs_components": (_int, [_vp, _vp, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "gs_fiedler": (_int, [_vp, _f64, _i32, ctypes.POINTER(_f64), ctypes.POINTER(_i32)]),
 }
+
+
+# entry points that touch no caller buffers on the device: no stream ordering
+_NO_ORDER = frozenset({"gs_set_stream", "gs_stream_wait", "gs_stream_signal", "gs_set_async",
+                       "gs_profile_enable", "gs_profile_reset", "gs_profile_get",
+                       "gs_graph_shape", "gs_synchronize"})
 
 
 class GsparseUnavailable(RuntimeError):
@@ -115,6 +124,8 @@ def check(rc: int, what: str = ""):
         raise ValueError(text)
     if rc == GS_EUNSUPPORTED:
         raise NotImplementedError(text)
+    if rc == GS_EINDEX:
+        raise IndexError(text)
     if rc == GS_ENOMEM:
         raise MemoryError(text)
     raise GsparseError(f"[{rc}] {text}")
@@ -163,6 +174,7 @@ class Context:
             raise GsparseUnavailable(f"gs_create(device={self.device}) failed: {msg}")
         self._h = h
         self._L = L
+        self._async = False
 
     @property
     def handle(self):
@@ -179,8 +191,35 @@ class Context:
         except Exception:
             pass
 
+    def _torch_stream(self):
+        """torch's current stream on this device, or None when torch has not
+        touched the GPU in this process (then no torch work can be pending)."""
+        try:
+            import torch
+        except ImportError:  # pragma: no cover - torch is a dependency
+            return None
+        if not torch.cuda.is_initialized():
+            return None
+        return torch.cuda.current_stream(self.device).cuda_stream
+
     def call(self, name: str, *args):
+        """Call a libgsparse entry point on this context.
+
+        Compute calls are ordered after torch's current stream first: device
+        buffers handed in (inputs torch just produced, or caching-allocator
+        blocks torch's stream last used) are ready before the library's own
+        stream touches them.  In async mode torch's stream is then ordered
+        after the library's, so device outputs are complete for torch too."""
+        ts = None if name in _NO_ORDER else self._torch_stream()
+        if ts is not None:
+            check(self._L.gs_stream_wait(self._h, ts), "gs_stream_wait")
         check(getattr(self._L, name)(self._h, *args), name)
+        if ts is not None and self._async:
+            check(self._L.gs_stream_signal(self._h, ts), "gs_stream_signal")
+
+    def set_async(self, on: bool):
+        self.call("gs_set_async", int(on))
+        self._async = bool(on)
 
     # ---- profiling -------------------------------------------------------
     def profile(self, on: bool = True):

@@ -138,6 +138,9 @@ def sharded_backbone(comm: Comm, edge_index: np.ndarray, num_nodes: int,
     """metric_backbone keep mask with the per-source searches split over ranks
     (source row u goes to rank u % world); one all-reduce(sum) of the keep
     bytes -- each column is decided by exactly one rank."""
+    from .metric_backbone import check_weights
+
+    check_weights(edge_weights, np.asarray(edge_index).shape[1])
     if mask_fn is None:
         from .metric_backbone import backbone_mask as mask_fn
     part = mask_fn(edge_index, num_nodes, edge_weights, epsilon, part=comm.rank,

@@ -33,6 +33,15 @@ def _context(ctx: Context | None) -> Context:
     return _CTX
 
 
+def check_weights(edge_weights, n_edges: int) -> None:
+    """The reference reads ``edge_weights[idx]`` for every edge_index column
+    (metric_backbone.py:73-74): fewer weights than columns is NumPy's
+    IndexError there, and must never reach the library as a short buffer."""
+    nw = len(edge_weights)
+    if nw < n_edges:
+        raise IndexError(f"index {nw} is out of bounds for axis 0 with size {nw}")
+
+
 def backbone_mask(edge_index: np.ndarray, num_nodes: int, edge_weights: np.ndarray,
                   epsilon: float = 1e-9, ctx: Context | None = None,
                   return_relax: bool = False, part: int = 0, nparts: int = 1):
@@ -46,12 +55,14 @@ def backbone_mask(edge_index: np.ndarray, num_nodes: int, edge_weights: np.ndarr
     E = ei.shape[1]
     src = np.ascontiguousarray(ei[0])
     dst = np.ascontiguousarray(ei[1])
-    w = np.ascontiguousarray(np.asarray(edge_weights, dtype=np.float64)[:E])
+    w = np.ascontiguousarray(np.asarray(edge_weights, dtype=np.float64).reshape(-1)[:E])
+    check_weights(w, E)
     keep = np.zeros(max(E, 1), dtype=np.uint8)
     relax = ctypes.c_int64(0)
     c = _context(ctx)
-    c.call("gs_metric_backbone_part", int(num_nodes), E, ptr(src), ptr(dst), ptr(w), GS_HOST,
-           float(epsilon), int(part), int(nparts), ptr(keep), GS_HOST, ctypes.byref(relax))
+    c.call("gs_metric_backbone_part", int(num_nodes), E, ptr(src), ptr(dst), ptr(w), len(w),
+           GS_HOST, float(epsilon), int(part), int(nparts), ptr(keep), GS_HOST,
+           ctypes.byref(relax))
     mask = keep[:E].view(bool)
     return (mask, relax.value) if return_relax else mask
 
@@ -77,10 +88,7 @@ def compute_metric_backbone(
         print(f"  Epsilon: {epsilon}")
 
     edge_weights = np.asarray(edge_weights)
-    if len(edge_weights) < n_edges:
-        # the reference indexes edge_weights[idx] for every column (:73-74)
-        raise IndexError(f"index {len(edge_weights)} is out of bounds for axis 0 with size "
-                         f"{len(edge_weights)}")
+    check_weights(edge_weights, n_edges)
     if verbose:
         m = rows < edge_index[1]
         und = len(np.unique(rows[m].astype(np.int64) * max(n_nodes, 1) + edge_index[1][m]))
@@ -135,13 +143,17 @@ def pair_distances(edge_index: np.ndarray, num_nodes: int, weights, pairs,
     ei = np.asarray(edge_index, dtype=np.int64)
     src = np.ascontiguousarray(ei[0])
     dst = np.ascontiguousarray(ei[1])
-    w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float64)[: ei.shape[1]]
+    w = None
+    if weights is not None:
+        w = np.ascontiguousarray(np.asarray(weights, dtype=np.float64).reshape(-1)[: ei.shape[1]])
+        check_weights(w, ei.shape[1])
     pr = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
     qs = np.ascontiguousarray(pr[:, 0])
     qt = np.ascontiguousarray(pr[:, 1])
     out = np.empty(len(pr), dtype=np.float64)
     c.call("gs_pair_distances", int(num_nodes), int(ei.shape[1]), ptr(src), ptr(dst),
-           ptr(w) if w is not None else None, GS_HOST, int(len(pr)), ptr(qs), ptr(qt), ptr(out))
+           ptr(w) if w is not None else None, 0 if w is None else len(w), GS_HOST, int(len(pr)),
+           ptr(qs), ptr(qt), ptr(out))
     return out
 
 

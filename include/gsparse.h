@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 1
+#define GS_API_VERSION 2
 
 enum {
     GS_OK = 0,
@@ -33,7 +33,9 @@ enum {
     GS_EHIP = -2,         /* HIP runtime error                                 */
     GS_ENOMEM = -3,       /* device allocation failed                          */
     GS_ESTATE = -4,       /* call out of order (e.g. no graph set)             */
-    GS_EUNSUPPORTED = -5  /* input outside the implemented contract            */
+    GS_EUNSUPPORTED = -5, /* input outside the implemented contract            */
+    GS_EINDEX = -6        /* an array shorter than the index range it must cover
+                             (Python shim raises IndexError, as NumPy does)     */
 };
 
 enum { GS_HOST = 0, GS_DEVICE = 1 };
@@ -50,6 +52,15 @@ void gs_destroy(gs_ctx *ctx);
 /* Use an external hipStream_t (e.g. torch.cuda.current_stream()); NULL =
  * the context's own stream. */
 int gs_set_stream(gs_ctx *ctx, void *hip_stream);
+/* Stream ordering without a host sync (hip_stream NULL = the null stream):
+ * gs_stream_wait -- work the context enqueues from now on runs after
+ *   everything already enqueued on hip_stream (call it before handing the
+ *   library device buffers that another stream produced or last used, e.g.
+ *   torch.cuda.current_stream());
+ * gs_stream_signal -- work enqueued on hip_stream from now on runs after
+ *   everything the context has enqueued (device outputs in async mode). */
+int gs_stream_wait(gs_ctx *ctx, void *hip_stream);
+int gs_stream_signal(gs_ctx *ctx, void *hip_stream);
 int gs_synchronize(gs_ctx *ctx);
 /* 1: device-pointer outputs may still be in flight on return. */
 int gs_set_async(gs_ctx *ctx, int async_);
@@ -150,7 +161,10 @@ int gs_topk_mask(gs_ctx *ctx, const double *scores, int s_loc, int64_t nnz, int6
  * keep[idx] for every edge_index column idx=(src,dst): shortest-path
  * distance d from src in the undirected graph of the src<dst columns
  * (min weight over duplicates), keep iff d == inf or w[idx] <= d + eps.
- * n_relax (optional) returns the number of edge relaxations performed. */
+ * nw = number of entries of w: nw < E is GS_EINDEX (the reference reads
+ * edge_weights[idx] for every column, metric_backbone.py:73-74, and raises
+ * IndexError).  n_relax (optional) returns the number of edge relaxations
+ * performed. */
 /* sparsify_degree_aware phase 1 (core.py:415-428, min_edges_per_node = 1):
  * for every node u, pick[u] = the edge_index column i (src[i] == u) holding
  * the unique maximum of scores[i], -1 if u has no column, -2 when the
@@ -162,27 +176,28 @@ int gs_segment_argmax(gs_ctx *ctx, const double *scores, int s_loc, int64_t nsco
                       int pick_loc);
 
 int gs_metric_backbone(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src,
-                       const int64_t *dst, const double *w, int loc, double eps,
+                       const int64_t *dst, const double *w, int64_t nw, int loc, double eps,
                        uint8_t *keep, int keep_loc, int64_t *n_relax);
 /* Part `part` of `nparts` of gs_metric_backbone (multi-GPU): keep
  * bytes of the columns whose source row u has u % nparts == part (their
  * searches run here), 0 elsewhere -- the element-wise sum over parts equals
  * the whole keep mask. */
 int gs_metric_backbone_part(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src,
-                            const int64_t *dst, const double *w, int loc, double eps, int part,
-                            int nparts, uint8_t *keep, int keep_loc, int64_t *n_relax);
+                            const int64_t *dst, const double *w, int64_t nw, int loc, double eps,
+                            int part, int nparts, uint8_t *keep, int keep_loc, int64_t *n_relax);
 
 /* Exact shortest-path distances for nq node pairs (qs[q], qt[q]) (host arrays;
  * out host) in the graph metric_backbone.py:70-79 builds from the columns
  * (src, dst, w): undirected, the columns with src < dst, weight the minimum
- * over duplicates; w == NULL: unit weights (hop counts).  +inf when
+ * over duplicates; w == NULL: unit weights (hop counts); nw = entries of w
+ * (nw < E: GS_EINDEX).  +inf when
  * unreachable; 0 when qs == qt.  Bit-identical to NetworkX Dijkstra's
  * left-fold path sums.  Replaces the nx.shortest_path_length calls of
  * verify_geodesic_preservation (metric_backbone.py:144-225) and
  * compute_geodesic_preservation (metrics.py:361-442). */
 int gs_pair_distances(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src, const int64_t *dst,
-                      const double *w, int loc, int64_t nq, const int64_t *qs, const int64_t *qt,
-                      double *out);
+                      const double *w, int64_t nw, int loc, int64_t nq, const int64_t *qs,
+                      const int64_t *qt, double *out);
 
 /* Exact effective resistance of the resident (symmetric) graph, one score per
  * CSR entry.  Replaces calculate_effective_resistance_scores (metrics.py:124-175:

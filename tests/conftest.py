@@ -5,6 +5,7 @@ C-ABI library loading/exports); `-m gpu` tests call libgsparse.so on an
 MI355X and compare with the oracle / golden vectors.
 """
 
+import faulthandler
 import glob
 import os
 import sys
@@ -23,6 +24,10 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and libgsparse.so")
+    # Python stacks of every thread on a fatal signal (SIGSEGV / SIGABRT inside
+    # the native library), written to the real stderr even under capture
+    if not faulthandler.is_enabled():
+        faulthandler.enable(all_threads=True)
 
 
 def golden_names(include_big=True):

@@ -260,6 +260,16 @@ def test_rmat14_vs_oracle(gs, rmat14):
     assert bits_equal(np.concatenate(parts), sp_.compute_scores("jaccard"))
 
 
+def _column_costs(ei, n):
+    """Jaccard costs (_scores_to_cost) per edge_index column: the CSR entry of
+    each column's (u, v), so graphs with duplicate columns get E weights."""
+    ip, ix, _ = O.canonical_csr(ei, n)
+    rows = np.repeat(np.arange(n), np.diff(ip))
+    cost_csr = O.scores_to_cost(O.jaccard(ip, ix), "jaccard")
+    pos = np.searchsorted(rows.astype(np.int64) * n + ix, ei[0].astype(np.int64) * n + ei[1])
+    return cost_csr[pos]
+
+
 def _hub_graph():
     """RMAT-14 plus hubs in every Jaccard row class of gs_jaccard.hip (LDS tables
     of 2K / 8K / 32K slots and the > 16384 bitmap rows), hub-hub edges and
@@ -356,11 +366,7 @@ def test_backbone_certificates_match_plain_search(gs, graph, monkeypatch):
         ei, n = _hub_graph()
     else:
         ei, n = graphs.roman_like(), 22662
-    ip, ix, _ = O.canonical_csr(ei, n)
-    rows = np.repeat(np.arange(n), np.diff(ip))
-    cost_csr = O.scores_to_cost(O.jaccard(ip, ix), "jaccard")
-    pos = np.searchsorted(rows.astype(np.int64) * n + ix, ei[0].astype(np.int64) * n + ei[1])
-    w = cost_csr[pos]
+    w = _column_costs(ei, n)
     keep = backbone_mask(ei, n, w)
     monkeypatch.setenv("GSPARSE_BB_LANDMARKS", "0")
     keep0 = backbone_mask(ei, n, w)
@@ -744,8 +750,9 @@ def test_backbone_multi_source_searches(gs, S, threads, monkeypatch):
     assert np.array_equal(backbone_mask(ei, n, cost[: ei.shape[1]]), O.metric_backbone(ei, n, cost))
     monkeypatch.setenv("GSPARSE_BB_LANDMARKS", "0")
     for ei, n in [(graphs.rmat(14, 8, seed=3), 1 << 14), _hub_graph()]:
-        ip, ix, _ = O.canonical_csr(ei, n)
-        w = O.scores_to_cost(O.jaccard(ip, ix), "jaccard")[: ei.shape[1]]
+        # one weight per column (the hub graph has duplicate columns, so its CSR
+        # has fewer entries than edge_index: index the CSR costs by column)
+        w = _column_costs(ei, n)
         multi = backbone_mask(ei, n, w)
         monkeypatch.setenv("GSPARSE_BB_MULTI", "1")
         single = backbone_mask(ei, n, w)

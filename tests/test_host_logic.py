@@ -121,3 +121,19 @@ def test_generators_are_deterministic_and_canonical():
     assert np.array_equal(r, load_golden("rmat10")["edge_index"])
     full = graphs.roman_like()
     assert full.shape == (2, 65854)
+
+
+def test_short_edge_weights_raise_index_error():
+    """metric_backbone.py:73-74 reads edge_weights[idx] for every column: fewer
+    weights than columns is an IndexError before anything reaches libgsparse
+    (host-only checks; the library re-checks the count it is given)."""
+    from gsparse.distributed import sharded_backbone
+    from gsparse.metric_backbone import check_weights
+
+    check_weights(np.zeros(5), 5)
+    check_weights(np.zeros(6), 5)
+    with pytest.raises(IndexError):
+        check_weights(np.zeros(4), 5)
+    ei = np.array([[0, 1, 1, 2], [1, 0, 2, 1]])
+    with pytest.raises(IndexError):
+        sharded_backbone(None, ei, 3, np.ones(3), mask_fn=lambda *a, **k: None)

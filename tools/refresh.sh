@@ -20,7 +20,7 @@ tail -1 "$O/prof_roman.log"
 if [ -n "${WITH_BACKBONE:-}" ]; then
   timeout -k 10 300 python bench.py --workload backbone --steps 1 --warmup 1 > "$O/backbone_rmat18_bench.json" 2> "$O/backbone_rmat18_bench.err" || { tail -5 "$O/backbone_rmat18_bench.err"; exit 1; }
   cat "$O/backbone_rmat18_bench.json"
-  bash tools/profile_bench.sh "$O/prof_backbone" --workload backbone > "$O/prof_backbone.log" 2>&1 || { tail -5 "$O/prof_backbone.log"; exit 1; }
+  bash tools/profile_bench.sh "$O/prof_backbone-rmat18" --workload backbone > "$O/prof_backbone.log" 2>&1 || { tail -5 "$O/prof_backbone.log"; exit 1; }
   tail -1 "$O/prof_backbone.log"
 fi
 if [ -n "${WITH_EXTRA:-}" ]; then
