@@ -1756,14 +1756,18 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         // Roman size, 2,674 columns: 0.51 s vs 0.53 s for mode 0; k/8 columns ~0.09 s vs 0.12 s.
         const bool resident = n > 10000 && n <= 24576 && ch.count >= 4 &&
                               er.lnnz <= kStoreQRowLen * n;
-        int mode = resident                                   ? 4
+        // register-resident solver (5) wherever its geometry fits the resident range
+        const bool regres = cg_regres_applies(n, ch.count, ch.len);
+        int mode = resident && regres                         ? 5
+                   : resident                                 ? 4
                    : (n > 0 && er.lnnz > kStoreQRowLen * n) ? 3
                    : ncols >= 2048                          ? 0
                    : ncols >= 512                           ? 1
                                                             : 3;
         if (const char *e = getenv("GSPARSE_CG_MODE")) {
             const int v = atoi(e);
-            mode = (v >= 0 && v <= 4) ? v : 0;
+            mode = (v >= 0 && v <= 5) ? v : 0;
+            if (mode == 5 && !regres) mode = 4;
         }
         if (const char *e = getenv("GSPARSE_CG_STOREQ")) mode = atoi(e) != 0 ? 1 : 0;
         const bool storeq = mode != 0;
@@ -1807,8 +1811,8 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         const int64_t *lp = er.lp.as<int64_t>();
         const int32_t *li = er.li.as<int32_t>();
         const double *lv = er.lv.as<double>();
-        if (mode == 4) {
-            // resident solver: one 1024-thread workgroup per CU, whole columns per workgroup
+        if (mode == 4 || mode == 5) {
+            // resident solvers: one workgroup per CU, whole columns per workgroup
             const int64_t ldn = (n + 7) & ~(int64_t)7;
             int64_t slots = 256;
             if (const char *e = getenv("GSPARSE_CG_SLOTS")) slots = atoi(e) > 0 ? atoi(e) : slots;
@@ -1842,6 +1846,21 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             const int32_t dcount = (unit & 3) == 3 ? 1 : 0;
             unit &= 1;
             if (const char *e = getenv("GSPARSE_RES_UNIT")) unit = unit && atoi(e) != 0;
+            long long *rprof = nullptr;
+            if (getenv("GSPARSE_RES_PROF"))
+                rprof = (long long *)c->buf("er_res_prof").ensure(8 * sizeof(long long));
+            hipEvent_t t0 = nullptr;
+            if (mode == 5) {
+                int32_t dc = dcount;
+                if (const char *e = getenv("GSPARSE_RES_DCOUNT")) dc = dc && atoi(e) != 0;
+                if (n) GS_HIP(hipMemsetAsync(cp.iters + col0, 0, sizeof(int32_t) * ncols, c->stream));
+                t0 = prof_begin(c);
+                if (n)
+                    cg_regres_solve(c, n, lp, li, lv, unit, dc, sdiag, Rr, er.ld, col0, ncols, maxiter,
+                                    rtol, ch.count, ch.a, ch.len, Xc, ldn, cp.iters, slots, rprof);
+                else
+                    GS_HIP(hipMemsetAsync(cp.iters + col0, 0, sizeof(int32_t) * ncols, c->stream));
+            } else {
             // longest row (the SELL block widths hold it) -> ELL width 4 / 8 / 12 / 16, else SELL
             int32_t maxw = 0;
             int sell_w = 8;
@@ -1886,9 +1905,6 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
                 k_sell_fill<<<grid_for(n, 256, 16384), 256, 0, c->stream>>>(
                     n, lp, li, lv, soff, swid, scol, sval);
             GS_HIP(hipGetLastError());
-            long long *rprof = nullptr;
-            if (getenv("GSPARSE_RES_PROF"))
-                rprof = (long long *)c->buf("er_res_prof").ensure(8 * sizeof(long long));
             ResArgs ra{n, er.ld, ldn, col0, ncols, lp, li, lv, Rr, Xc, sl, ca, cl, maxiter, rtol,
                        cp.iters, soff, swid, scol, sval, sdiag, ecol, evalp, lde, 0, 0, rprof,
                        dcount};
@@ -1904,7 +1920,7 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             if (const char *e = getenv("GSPARSE_RES_QLDS")) qlmax = atoi(e) ? qlmax : 0;
             ra.ql = n < qlmax ? n : qlmax;
             const size_t dyn = sizeof(double) * (size_t)ra.ql + 8 * (size_t)ra.nstab + 8;
-            hipEvent_t t0 = prof_begin(c);
+            t0 = prof_begin(c);
 #define GS_RES(B, W, C, U, E)                                                                  \
     do {                                                                                        \
         GS_HIP(hipFuncSetAttribute((const void *)k_cg_resident<B, W, C, U, E>,                  \
@@ -1939,6 +1955,7 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             }
 #undef GS_RES_U
 #undef GS_RES
+            }
             GS_HIP(hipGetLastError());
             prof_end(c, t0, "cg_res", 0.0);
             const bool prof_rec = c->profiling && !c->pending.empty();

@@ -174,6 +174,16 @@ void sort_pairs_u64_i64(gs_ctx *c, uint64_t *keys, int64_t *vals, int64_t n, int
 // Graph helpers used by the ER path (gs_graph.hip)
 void ensure_transpose(gs_ctx *c);
 
+// Register-resident CG (ApproxER mode 5, gs_cg_reg.hip): applies when the T BLAS
+// chunks (lengths len[t]) fit its thread geometry; solves columns [col0, col0+ncols)
+// of L_reg (CSR lp/li/lv) into Xc (column-major, ldn per column)
+bool cg_regres_applies(int64_t n, int T, const int64_t *len);
+void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li, const double *lv,
+                     int unit, int dcount, const double *diag, const double *Rr, int64_t ld,
+                     int64_t col0, int64_t ncols, int32_t maxiter, double rtol, int T,
+                     const int64_t *ha, const int64_t *hlen, double *Xc, int64_t ldn,
+                     int32_t *iters, int64_t slots, long long *prof);
+
 // Whole-graph Jaccard of a symmetric graph (gs_jaccard.hip)
 // counts != 0: |N(u) ∩ N(v)| per entry instead of the Jaccard ratio
 void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts = 0);

@@ -59,11 +59,12 @@ def test_approx_er_bit_exact(gs, name):
     assert bits_equal(er, ref), float(np.max(np.abs(er - ref) / np.abs(ref)))
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4"])
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4", "5"])
 @pytest.mark.parametrize("name", ["karate_csr", "rmat10", "directed_dup", "roman2000"])
 def test_approx_er_all_cg_modes(gs, name, mode, monkeypatch):
     """q recomputed in the update kernel (0), stored by the fused p/q kernel (1),
-    split p stream + SpMV (2, 3), or the resident per-column solver (4) -- the
+    split p stream + SpMV (2, 3), the resident per-column solver (4), or the
+    register-resident one (5: one BLAS chunk here, 8 threads per chain) -- the
     same bits in every mode."""
     monkeypatch.setenv("GSPARSE_CG_MODE", mode)
     g = load_golden(name)
@@ -110,10 +111,19 @@ def chunked_er():
                                   "GSPARSE_RES_UNIT": "0"},
                                  {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_DCOUNT": "0"},
                                  {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_RBW": "26"},
-                                 {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_RBW": "28"}],
+                                 {"GSPARSE_CG_MODE": "4", "GSPARSE_RES_RBW": "28"},
+                                 {"GSPARSE_CG_MODE": "5"},
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_RES_UNIT": "0"},
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_RES_DCOUNT": "0"},
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_CG_SLOTS": "7"},
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_KEEP": "40"},
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_KEEP": "0",
+                                  "GSPARSE_RES_UNIT": "0"}],
                          ids=["m0", "m1", "m3", "m4", "m4-ell", "m4-q-global", "m4-7slots",
                               "m4-weighted-sell", "m4-weighted-ell", "m4-slices-global",
-                              "m4-rb4w4", "m4-rb4w4-weighted", "m4-diag-loaded", "m4-w6", "m4-w8"])
+                              "m4-rb4w4", "m4-rb4w4-weighted", "m4-diag-loaded", "m4-w6", "m4-w8",
+                              "m5", "m5-weighted", "m5-diag-loaded", "m5-7slots", "m5-p-global",
+                              "m5-p-all-global-weighted"])
 @pytest.mark.parametrize("threads", [3, 8])
 @pytest.mark.parametrize("graph", ["unit", "dup", "hub"])
 def test_approx_er_blas_chunks_vs_oracle(gs, chunked_er, graph, threads, env, monkeypatch):
@@ -128,7 +138,7 @@ def test_approx_er_blas_chunks_vs_oracle(gs, chunked_er, graph, threads, env, mo
     assert bits_equal(er, ref[threads])
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "3", "4"])
+@pytest.mark.parametrize("mode", ["0", "1", "3", "4", "5"])
 def test_er_column_blocks_in_every_mode(gs, chunked_er, mode, monkeypatch):
     """A rank's column block [col0, col1) (the N-GPU split) solved alone, in the
     batched and the resident solver: the blocks' partial sums, added along the
