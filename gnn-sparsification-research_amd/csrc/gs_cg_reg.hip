@@ -1,456 +1,9 @@
-// gs_cg_reg.hip -- register-resident CG (ApproxER mode 5), metrics.py:284-289.
-//
-// The k JL columns are independent CG solves of L_reg z = y (SciPy 1.15 cg,
-// maxiter 500, rtol 1e-6) whose dot products follow OpenBLAS-SkylakeX ddot's
-// order for T threads: T contiguous chunks, in each 32 FMA accumulator
-// chains (chain j: rows a_t + j, a_t + j + 32, ...), then a fixed fold, a
-// 16-row block and an FMA tail (gs_er.hip chunk_dot).
-//
-// Mode 4 (k_cg_resident) keeps a column's r, p, q, x in Infinity-Cache-
-// resident slots and streams ~2 MB through each CU per column-iteration; its
-// bound is the CU's memory pipeline.  Here one 512-thread workgroup per CU
-// owns a column and keeps it ON the CU:
-//   * r and x of every row live in registers: thread (chain, g) owns the rows
-//     s = g, g + G, g + 2G, ... of its chain (G threads per chain, the rows of a
-//     chain dealt round-robin), so a wave's 64 lanes touch 64 consecutive rows;
-//   * p lives in LDS (a prefix of every BLAS chunk's rows, sized so the chunks
-//     share the LDS in proportion; the rest in a per-workgroup global slot,
-//     L2-resident, gathered under a wave-uniform branch);
-//   * q is never stored: L_reg p is recomputed per row where it is needed
-//     (the p.q pass and the r update), from an ELL-8 copy of L_reg with
-//     uint16 columns (16 B per row, one load, shared by all CUs through L2);
-//   * a dot's chain (t, j) is folded by its g = 0 lane in row order: at step u
-//     it takes the G rows s = G u .. G u + G - 1 from its own and its partner
-//     lanes (shuffles), so the FMA sequence is exactly OpenBLAS's;
-//   * every wave finishes every dot itself (chunk fold + 16-block + tail,
-//     then the chunks in order) from LDS, so the result needs no broadcast.
-// Per column-iteration the memory traffic is the ELL reads (L2) and the p
-// rows that do not fit LDS; everything else is LDS and registers.
-#include <algorithm>
-
-#include "gs_internal.hpp"
+// gs_cg_reg.hip -- host side of the register-resident CG (ApproxER mode 5): the
+// ELL-8 copy of L_reg with p codes, the LDS plan, geometry and launch.  The kernel
+// and its design notes are in gs_cg_reg.hpp.
+#include "gs_cg_reg.hpp"
 
 namespace gs {
-
-static constexpr int kRegThreads = 512;
-static constexpr int kRegMaxChunks = kRegThreads / 32;  // 32 chains per chunk
-static constexpr int kPre = 4;  // slots a thread's ELL row / p_old loads run ahead
-
-struct RegArgs {
-    int64_t ld, ldn, col0, ncols;
-    int32_t n;
-    const double *Rr;     // b = Y, row-major (stride ld)
-    double *Xc;           // x out: column col0 + i at Xc + i * ldn
-    double *pg;           // per-workgroup p rows not held in LDS (ldn each)
-    const uint4 *ell;     // [n]: the first 8 entries of each row as p codes (uint16, ascending
-                          // columns; padding: zslot), see k_ell8_fill
-    const double *ellv;   // [n][8] weights (weighted form), else nullptr
-    const uint16_t *rlen; // [n] entries of each row of L_reg
-    const int64_t *optr;  // [n+1] entries 9.. of longer rows
-    const uint16_t *ocol;  // p codes
-    const double *oval;
-
-    int32_t zslot;        // LDS slot after the p rows: holds 0.0, the ELL padding code
-    int32_t maxiter;
-    double rtol;
-    int32_t *iters;       // [k] iterations executed per column
-    int32_t T;            // BLAS chunks
-    const int64_t *ca, *cl;  // chunk starts / lengths (device)
-    const int64_t *ck, *cb;  // rows of each chunk whose p is in LDS (a prefix), and their LDS base
-    long long *prof;      // optional: workgroup 0's phase times
-};
-
-__device__ __forceinline__ double reg_uniform(double v) {
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
-// G threads per chain (power of two), R row slots per thread, UNIT: every
-// off-diagonal weight is -1.0 and every diagonal one fl((entries - 1) + 1e-6) (no
-// weights loaded; q_i folds -p_j and dg * p_i); else the ELL carries the weights
-template <int G, int R, bool UNIT>
-__global__ void __launch_bounds__(kRegThreads) k_cg_regres(RegArgs A) {
-    constexpr int CW = 64 / G;  // chains per wave
-    extern __shared__ double lds[];
-    const int T = A.T, nch = 32 * T;
-    // LDS: p at offset 0 (a gather's address is its code * 8), the zero and scratch
-    // slots, then chain sums, tail rows and the chunk table
-    double *sp = lds;
-    double *acc_pq = lds + A.zslot + 2, *acc_rr = acc_pq + nch;
-    double *side_p = acc_pq + 2 * nch, *side_q = acc_pq + 3 * nch, *side_r = acc_pq + 4 * nch;
-    double *side_x = acc_pq + 5 * nch;  // tail rows' r lives in side_r, x here
-    // [4][kRegMaxChunks]: starts, lengths, LDS-resident prefix, its LDS base
-    int *s_ch = reinterpret_cast<int *>(acc_pq + 6 * nch);
-    const int tid = threadIdx.x, lane = tid & 63;
-    if (tid < T) {
-        s_ch[tid] = (int)A.ca[tid];
-        s_ch[kRegMaxChunks + tid] = (int)A.cl[tid];
-        s_ch[2 * kRegMaxChunks + tid] = (int)A.ck[tid];
-        s_ch[3 * kRegMaxChunks + tid] = (int)A.cb[tid];
-    }
-    __syncthreads();
-    const int jj = lane % CW, g = lane / CW;
-    const int chain = (tid >> 6) * CW + jj;
-    const bool live = chain < nch;
-    const int t = live ? chain >> 5 : 0, j = chain & 31;
-    const int L = s_ch[kRegMaxChunks + t];
-    const int n32 = L & ~31;
-    const int S = live ? n32 >> 5 : -1;  // chain rows; row s == S is a tail row when j < tl
-    const int tl = L - n32;
-    int base = s_ch[t] + j + 32 * g;  // row of slot u: base + 32 G u
-    // register slots u < uc hold chain rows; the chunk's tail row s == S (j < tl) is
-    // kept by the g == 0 lane with its r and x in LDS (side_r / side_x)
-    int uc = S > g ? (S - g + G - 1) / G : 0;
-    const bool tail = live && g == 0 && j < tl;
-    const int trow = s_ch[t] + n32 + j;
-    const int tix = t * 32 + j;
-    int Sv = S;
-    // Re-derive the per-slot rows and conditions inside every phase: left loop-
-    // invariant, the compiler hoists all R of them out of the iteration loop and
-    // keeps them live (hundreds of SGPRs/VGPRs, spilled to scratch).
-    auto launder = [&]() { asm volatile("" : "+v"(base), "+v"(uc), "+v"(Sv)); };
-    const int ca_t = s_ch[t], keep_t = s_ch[2 * kRegMaxChunks + t], lbase_t = s_ch[3 * kRegMaxChunks + t];
-    const int zslot = A.zslot;  // LDS slot holding 0.0 (the ELL padding code)
-    // explicit address spaces: a select between an LDS and a global pointer would
-    // become one (slow) flat load
-    typedef __attribute__((address_space(3))) double lds_f64;
-    lds_f64 *spl = (lds_f64 *)sp;
-    double *pgw = A.pg + (int64_t)blockIdx.x * A.ldn;
-    // rows of p outside LDS: raw buffer, offsets past its size read 0 / drop the store
-    const __amdgpu_buffer_rsrc_t prs =
-        __builtin_amdgcn_make_buffer_rsrc(pgw, 0, (int)(A.ldn * 8), 0x00020000);
-    constexpr int kOob = (int)0x80000000;
-    if (tid == 0) spl[zslot] = 0.0;
-
-    // p of a row lives at its code: an LDS slot (< 0x8000) or 0x8000 | row (global);
-    // code_of takes a row of this lane's chunk
-    auto code_of = [&](int row) {
-        const int o = row - ca_t;
-        return o < keep_t ? lbase_t + o : 0x8000 | row;
-    };
-    // LDS access always; the global one only under a wave-uniform branch (a wave's
-    // rows of one slot are 32 G consecutive rows of a chunk, mostly all LDS-resident)
-    auto ldc = [&](int cd) -> double {
-        double v = spl[cd < 0x8000 ? cd : zslot];
-        if (__builtin_amdgcn_ballot_w64(cd >= 0x8000)) {
-            const double vg = __builtin_bit_cast(
-                double, __builtin_amdgcn_raw_buffer_load_b64(prs, cd < 0x8000 ? kOob : (cd & 0x7fff) * 8, 0, 0));
-            v = cd < 0x8000 ? v : vg;
-        }
-        return v;
-    };
-    auto stc = [&](int cd, double v) {
-        spl[cd < 0x8000 ? cd : zslot + 1] = v;  // zslot + 1: a scratch slot
-        if (__builtin_amdgcn_ballot_w64(cd >= 0x8000))
-            __builtin_amdgcn_raw_buffer_store_b64(
-                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), prs,
-                cd < 0x8000 ? kOob : (cd & 0x7fff) * 8, 0, 0);
-    };
-    auto valid = [&](int u) { return u < uc; };
-    const uint32_t pad2 = (uint32_t)zslot | ((uint32_t)zslot << 16);
-    auto ell_row = [&](int u) -> uint4 {
-        return valid(u) ? A.ell[base + 32 * G * u] : make_uint4(pad2, pad2, pad2, pad2);
-    };
-    auto len_row = [&](int u) -> int { return valid(u) ? (int)A.rlen[base + 32 * G * u] : 0; };
-    auto rowof = [&](int u) { return base + 32 * G * u; };
-
-    // q_i = (L_reg p)_i, SciPy csr_matvec: fold from 0.0 in ascending column, products
-    // rounded; pown receives p_i.  Entries are p codes.  Unit form: off-diagonal
-    // products are -p_j exactly (-1.0 * x == -x) and the diagonal one fl(dg * p_i).
-    // Padding entries gather the zero slot: +-0.0 terms, and acc + (+-0.0) == acc bit
-    // for bit (acc starts at +0.0 and is never -0.0).  Codes of global rows read past
-    // the LDS (no fault; the value is replaced under one wave-uniform branch), so the
-    // slot issues no memory load whose result it waits for -- the ELL rows prefetched
-    // for the next slots stay in flight.
-    auto spmv = [&](int row, const uint4 e, int len, double &pown) -> double {
-        const int self = code_of(row);
-        const uint32_t w4[4] = {e.x, e.y, e.z, e.w};
-        int cd[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) cd[k] = (int)((w4[k >> 1] >> (16 * (k & 1))) & 0xffffu);
-        double pv[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) pv[k] = spl[cd[k]];
-        pown = spl[self];
-        const bool anyg = ((w4[0] | w4[1] | w4[2] | w4[3]) & 0x80008000u) != 0 || self >= 0x8000;
-        if (__builtin_amdgcn_ballot_w64(anyg)) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const bool gk = cd[k] >= 0x8000;
-                const double vg = __builtin_bit_cast(
-                    double, __builtin_amdgcn_raw_buffer_load_b64(prs, gk ? (cd[k] & 0x7fff) * 8 : kOob, 0, 0));
-                pv[k] = gk ? vg : pv[k];
-            }
-            pown = ldc(self);
-        }
-        double acc = 0.0, td = 0.0;
-        if (UNIT) {
-            const double dg = (double)(len - 1) + 1e-6;  // UNIT: L_reg_ii == fl((entries - 1) + 1e-6)
-            td = dg * pown;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const double v = cd[k] == self ? td : -pv[k];
-                acc = acc + v;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const double prod = A.ellv[(int64_t)row * 8 + k] * pv[k];
-                acc = acc + prod;
-            }
-        }
-        if (__builtin_amdgcn_ballot_w64(len > 8)) {  // rows longer than 8 entries: ocol / oval
-            const int64_t o0 = len > 8 ? A.optr[row] : 0, o1 = len > 8 ? A.optr[row + 1] : 0;
-            for (int64_t q = o0; q < o1; ++q) {
-                const int cc = (int)A.ocol[q];
-                const double pc = ldc(cc);
-                double v;
-                if (UNIT) v = cc == self ? td : -pc;
-                else v = A.oval[q] * pc;
-                acc = acc + v;
-            }
-        }
-        return acc;
-    };
-
-    // one step of every chain: rows s = G u + gg (gg < G) in order, folded by the g = 0 lane
-    auto chain_step = [&](double &acc, double av, double bv, int u) {
-        double as[G], bs[G];
-        as[0] = av;  // the folding lane's own row (g = 0)
-        bs[0] = bv;
-#pragma unroll
-        for (int gg = 1; gg < G; ++gg) {
-            as[gg] = __shfl(av, jj + CW * gg, 64);
-            bs[gg] = __shfl(bv, jj + CW * gg, 64);
-        }
-#pragma unroll
-        for (int gg = 0; gg < G; ++gg)
-            if (G * u + gg < Sv) acc = __builtin_fma(as[gg], bs[gg], acc);
-        // fold now: deferred, every slot's shuffled operands would stay live to the end
-        asm volatile("" : "+v"(acc));
-    };
-
-    // OpenBLAS finish of one dot (every wave computes it; lane = chunk)
-    auto finish = [&](const double *acc32all, const double *xa_all, const double *xb_all) -> double {
-        double d = 0.0;
-        if (lane < T) {
-            const int Lt = s_ch[kRegMaxChunks + lane];
-            const int n1 = Lt & ~15, n32t = n1 & ~31;
-            const double *a32 = acc32all + lane * 32;
-            const double *xa = xa_all + lane * 32, *xb = xb_all + lane * 32;
-            double dot = 0.0;
-            if (n1) {
-                // b[4q + l] = acc[8q + l] + acc[8q + 4 + l] (+ the 16-block row 4q + l),
-                // c4[l] = ((b[l] + b[4 + l]) + b[8 + l]) + b[12 + l] -- one l at a time
-                const bool blk = n1 > n32t;
-                double c4[4];
-                for (int l = 0; l < 4; ++l) {
-                    double cl = 0.0;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        double b = a32[8 * q + l] + a32[8 * q + 4 + l];
-                        if (blk) b = __builtin_fma(xa[4 * q + l], xb[4 * q + l], b);
-                        cl = q == 0 ? b : cl + b;
-                    }
-                    c4[l] = cl;
-                }
-                dot = (c4[0] + c4[2]) + (c4[1] + c4[3]);
-            }
-            for (int i = 0; i < 15; ++i)
-                if (n1 + i < Lt) {
-                    const int ix = n1 - n32t + i;
-                    dot = __builtin_fma(xb[ix], xa[ix], dot);
-                }
-            d = dot;
-        }
-        if (T == 1) return reg_uniform(__shfl(d, 0, 64));
-        double total = 0.0;
-        for (int tt = 0; tt < T; ++tt) total = total + __shfl(d, tt, 64);
-        return reg_uniform(total);
-    };
-
-    long long tp[5] = {0, 0, 0, 0, 0};
-    long long tmark = wall_clock64();
-    auto lap = [&](int ph) {
-        const long long tn = wall_clock64();
-        tp[ph] += tn - tmark;
-        tmark = tn;
-    };
-
-    for (int64_t ci = blockIdx.x; ci < A.ncols; ci += gridDim.x) {
-        const int64_t c = A.col0 + ci;
-        double r[R], x[R];
-        // r = b.copy(); rho_0 = b.b
-        {
-            launder();
-            double acc = 0.0;
-#pragma unroll
-            for (int u = 0; u < R; ++u) {
-                x[u] = 0.0;
-                r[u] = valid(u) ? A.Rr[(int64_t)rowof(u) * A.ld + c] : 0.0;
-                chain_step(acc, r[u], r[u], u);
-            }
-            if (g == 0 && live) acc_rr[chain] = acc;
-            if (tail) {
-                side_r[tix] = A.Rr[(int64_t)trow * A.ld + c];
-                side_x[tix] = 0.0;
-            }
-        }
-        __syncthreads();
-        double rr = finish(acc_rr, side_r, side_r);
-        const double bn = __builtin_sqrt(rr);
-        const double atol = A.rtol * bn;  // max(atol=0, rtol*bnrm2)
-        int32_t done = 0;
-        double rho_prev = 0.0, alpha_prev = 0.0;
-        const bool act = !(bn == 0.0) && !(__builtin_sqrt(rr) < atol);
-        for (int32_t it = 0; act && it < A.maxiter; ++it) {
-            if (it > 0 && __builtin_sqrt(rr) < atol) break;  // loop-top test
-            const double rho_cur = rr;
-            const double beta = it > 0 ? rho_cur / rho_prev : 0.0;
-            lap(4);
-            // p = beta p + r (two roundings); x += alpha_{it-1} p_{it-1} rides along
-            launder();
-            if (it == 0) {
-#pragma unroll
-                for (int u = 0; u < R; ++u)
-                    if (valid(u)) stc(code_of(rowof(u)), r[u]);
-            } else {
-                double pb4[R];  // p_old, kPre slots ahead (each slot reads and writes only its row)
-#pragma unroll
-                for (int u = 0; u < kPre && u < R; ++u) pb4[u] = valid(u) ? ldc(code_of(rowof(u))) : 0.0;
-#pragma unroll
-                for (int u = 0; u < R; ++u) {
-                    if (u + kPre < R) pb4[u + kPre] = valid(u + kPre) ? ldc(code_of(rowof(u + kPre))) : 0.0;
-                    if (valid(u)) {
-                        const double po = pb4[u];
-                        const double t1 = alpha_prev * po;
-                        x[u] = x[u] + t1;
-                        const double pb = po * beta;
-                        stc(code_of(rowof(u)), pb + r[u]);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            if (tail) {
-                if (it == 0) {
-                    stc(code_of(trow), side_r[tix]);
-                } else {
-                    const double po = ldc(code_of(trow));
-                    const double t1 = alpha_prev * po;
-                    side_x[tix] = side_x[tix] + t1;
-                    const double pb = po * beta;
-                    stc(code_of(trow), pb + side_r[tix]);
-                }
-            }
-            __syncthreads();
-            lap(0);
-            // q = L_reg p and the chains of p.q
-            {
-                launder();
-                double acc = 0.0;
-                uint4 eb[R];  // ELL rows and lengths, kPre slots ahead
-                int lb[R];
-#pragma unroll
-                for (int u = 0; u < kPre && u < R; ++u) {
-                    eb[u] = ell_row(u);
-                    lb[u] = len_row(u);
-                }
-#pragma unroll
-                for (int u = 0; u < R; ++u) {
-                    if (u + kPre < R) {
-                        eb[u + kPre] = ell_row(u + kPre);
-                        lb[u + kPre] = len_row(u + kPre);
-                    }
-                    double pv = 0.0, qv = 0.0;
-                    if (valid(u)) qv = spmv(rowof(u), eb[u], lb[u], pv);
-                    chain_step(acc, pv, qv, u);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                if (g == 0 && live) acc_pq[chain] = acc;
-                if (tail) {
-                    double pt;
-                    side_q[tix] = spmv(trow, A.ell[trow], (int)A.rlen[trow], pt);
-                    side_p[tix] = pt;
-                }
-            }
-            __syncthreads();
-            lap(1);
-            const double pq = finish(acc_pq, side_p, side_q);
-            const double alpha = rho_cur / pq;
-            lap(2);
-            // r -= alpha q (q recomputed), chains of r.r
-            {
-                launder();
-                double acc = 0.0;
-                uint4 eb[R];
-                int lb[R];
-#pragma unroll
-                for (int u = 0; u < kPre && u < R; ++u) {
-                    eb[u] = ell_row(u);
-                    lb[u] = len_row(u);
-                }
-#pragma unroll
-                for (int u = 0; u < R; ++u) {
-                    if (u + kPre < R) {
-                        eb[u + kPre] = ell_row(u + kPre);
-                        lb[u + kPre] = len_row(u + kPre);
-                    }
-                    if (valid(u)) {
-                        double pu;
-                        const double t2 = alpha * spmv(rowof(u), eb[u], lb[u], pu);
-                        r[u] = r[u] - t2;
-                    }
-                    chain_step(acc, r[u], r[u], u);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                if (g == 0 && live) acc_rr[chain] = acc;
-                if (tail) {
-                    double pt;
-                    const double t2 = alpha * spmv(trow, A.ell[trow], (int)A.rlen[trow], pt);
-                    side_r[tix] = side_r[tix] - t2;
-                }
-            }
-            __syncthreads();
-            lap(3);
-            rr = finish(acc_rr, side_r, side_r);
-            rho_prev = rho_cur;
-            alpha_prev = alpha;
-            done = it + 1;
-        }
-        // x: b (||b|| == 0), 0 (no iteration), or the last pending update
-        launder();
-        double *xo = A.Xc + ci * A.ldn;
-#pragma unroll
-        for (int u = 0; u < R; ++u)
-            if (valid(u)) {
-                const int row = rowof(u);
-                double v;
-                if (bn == 0.0) v = r[u];
-                else if (done == 0) v = 0.0;
-                else {
-                    const double t1 = alpha_prev * ldc(code_of(row));
-                    v = (done > 1 ? x[u] : 0.0) + t1;
-                }
-                xo[row] = v;
-            }
-        if (tail) {
-            double v;
-            if (bn == 0.0) v = side_r[tix];
-            else if (done == 0) v = 0.0;
-            else {
-                const double t1 = alpha_prev * ldc(code_of(trow));
-                v = (done > 1 ? side_x[tix] : 0.0) + t1;
-            }
-            xo[trow] = v;
-        }
-        if (tid == 0) A.iters[c] = done;
-        __syncthreads();  // the next column's b.b chains reuse acc_rr / side_r
-    }
-    if (A.prof && blockIdx.x == 0 && tid == 0)
-        for (int i = 0; i < 5; ++i) A.prof[i] = tp[i];
-}
 
 // ELL-8 copy of L_reg: overflow entry counts (rows longer than 8)
 __global__ void k_ell8_count(int32_t n, const int64_t *__restrict__ lp, int64_t *__restrict__ cnt,
@@ -473,8 +26,24 @@ __device__ __forceinline__ uint32_t p_code(int32_t c, int T, const int64_t *__re
                                           : 0x8000u | (uint32_t)c;
 }
 
+// diagonal slot index (2 tid + parity) of row c in k_cg_regres (G threads per chain):
+// chain row s of chain (t, j) is slot s / G of thread g = s % G; a chunk's tail rows
+// belong to g = 0 with parity 0
+__device__ __forceinline__ int row_dslot(int32_t c, int T, const int64_t *__restrict__ tab, int G) {
+    int t = 0;
+    while (t + 1 < T && c >= tab[t + 1]) ++t;
+    const int o = (int)(c - tab[t]), n32 = (int)(tab[kRegMaxChunks + t] & ~(int64_t)31);
+    const bool in = o < n32;
+    const int j = in ? (o & 31) : o - n32, g = in ? (o >> 5) % G : 0;
+    const int par = in ? ((o >> 5) / G) & 1 : 0;
+    const int chain = t * 32 + j, CW = 64 / G;
+    return 2 * ((chain / CW) * 64 + (chain % CW) + CW * g) + par;
+}
+
+// dslot0 >= 0 (unit form): the diagonal entry's code is the owner thread's diagonal
+// slot dslot0 + tid instead of the row's p code
 __global__ void k_ell8_fill(int32_t n, int T, const int64_t *__restrict__ tab, uint32_t pad,
-                            const int64_t *__restrict__ lp,
+                            int G, int32_t dslot0, const int64_t *__restrict__ lp,
                             const int32_t *__restrict__ li, const double *__restrict__ lv,
                             const int64_t *__restrict__ optr, uint4 *__restrict__ ell,
                             double *__restrict__ ellv, uint16_t *__restrict__ ocol,
@@ -482,35 +51,50 @@ __global__ void k_ell8_fill(int32_t n, int T, const int64_t *__restrict__ tab, u
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e0 = lp[i], len = lp[i + 1] - e0;
+        const uint32_t dcode = dslot0 >= 0 ? (uint32_t)(dslot0 + row_dslot((int32_t)i, T, tab, G)) : 0u;
+        auto code = [&](int64_t e) -> uint32_t {
+            return (dslot0 >= 0 && li[e] == i) ? dcode : p_code(li[e], T, tab);
+        };
         uint32_t w[4] = {0, 0, 0, 0};
         for (int k = 0; k < 8; ++k) {
-            const uint32_t cc = k < len ? p_code(li[e0 + k], T, tab) : pad;
+            const uint32_t cc = k < len ? code(e0 + k) : pad;
             w[k >> 1] |= cc << (16 * (k & 1));
             if (ellv) ellv[i * 8 + k] = k < len ? lv[e0 + k] : 0.0;
         }
         ell[i] = make_uint4(w[0], w[1], w[2], w[3]);
         for (int64_t k = 8; k < len; ++k) {
-            ocol[optr[i] + k - 8] = (uint16_t)p_code(li[e0 + k], T, tab);
+            ocol[optr[i] + k - 8] = (uint16_t)code(e0 + k);
             if (oval) oval[optr[i] + k - 8] = lv[e0 + k];
         }
     }
 }
 
-// threads per chain for T chunks (power of two, 32 T G <= 512, G <= 8) and register
-// row slots per thread (the chain rows), 0 when the solver does not apply
-static int reg_geometry(int T, const int64_t *len, int &G) {
-    if (T < 1 || T > kRegMaxChunks) return -1;
+// threads per chain for T chunks on an NT-thread workgroup (power of two, 32 T G <= NT,
+// G <= 8) and register row slots per thread (the chain rows); -1 when it does not apply
+static int reg_geometry(int NT, int T, const int64_t *len, int &G) {
+    if (T < 1 || 32 * T > NT) return -1;
     G = 1;
-    while (G < 8 && 32 * T * (2 * G) <= kRegThreads) G *= 2;
+    while (G < 8 && 32 * T * (2 * G) <= NT) G *= 2;
     int64_t smax = 0;
     for (int t = 0; t < T; ++t) smax = std::max<int64_t>(smax, (len[t] & ~(int64_t)31) >> 5);
     return (int)((smax + G - 1) / G);
 }
 
+// workgroup size and slots: 256 threads (one wave per SIMD, 512 registers per lane)
+// where the slots fit 88, else 512 threads (two waves per SIMD) with up to 44
+static bool reg_pick(int64_t n, int T, const int64_t *len, int &NT, int &G, int &R) {
+    if (n <= 0 || n >= 0x8000) return false;
+    int g = 0;
+    const int r = reg_geometry(256, T, len, g);
+    if (r < 0 || r > 88) return false;
+    NT = 256, G = g;
+    R = r <= 24 ? 24 : r <= 48 ? 48 : r <= 64 ? 64 : 88;
+    return true;
+}
+
 bool cg_regres_applies(int64_t n, int T, const int64_t *len) {
-    int G = 0;
-    const int rneed = reg_geometry(T, len, G);
-    return n > 0 && n < 0x8000 && rneed >= 0 && rneed <= 44;
+    int NT, G, R;
+    return reg_pick(n, T, len, NT, G, R);
 }
 
 void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li, const double *lv,
@@ -519,9 +103,8 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
                      const int64_t *ha, const int64_t *hlen, double *Xc, int64_t ldn,
                      int32_t *iters, int64_t slots, long long *prof) {
     hipStream_t s = c->stream;
-    int G = 0;
-    const int rneed = reg_geometry(T, hlen, G);
-    GS_CHECK(rneed >= 0 && rneed <= 44 && n < 0x8000, GS_EUNSUPPORTED,
+    int NT = 0, G = 0, rsel = 0;
+    GS_CHECK(reg_pick(n, T, hlen, NT, G, rsel), GS_EUNSUPPORTED,
              "register-resident CG: n=%lld, %d chunks out of range", (long long)n, T);
     // ELL-8 copy (uint16 columns), overflow entries in CSR form
     auto *ocnt = (int64_t *)c->buf("er_reg_ocnt").ensure(sizeof(int64_t) * (n + 1));
@@ -537,7 +120,8 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     // slots, 6 x 32 T doubles of chain sums / tail rows, the chunk table
     const int nch = 32 * T;
     const size_t lds_max = 160 * 1024;
-    const int64_t cap = (int64_t)((lds_max - (6 * (size_t)nch + 2 * kRegMaxChunks + 2) * 8) / 8);
+    const int64_t cap =
+        (int64_t)((lds_max - (6 * (size_t)nch + 2 * kRegMaxChunks + 2 + 2 * NT) * 8) / 8);
     // prefixes in proportion to the chunk lengths, whole wave-slots (32 G rows) when
     // they cannot all fit
     int64_t keep[kRegMaxChunks], lbase[kRegMaxChunks], tot = 0;
@@ -553,7 +137,8 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
         zs += keep[t];
     }
     const uint32_t pad = (uint32_t)zs;  // the zero slot
-    const size_t dyn = sizeof(double) * ((size_t)zs + 2 + 6 * (size_t)nch + 2 * kRegMaxChunks);
+    const size_t dyn =
+        sizeof(double) * ((size_t)zs + 2 + 2 * NT + 6 * (size_t)nch + 2 * kRegMaxChunks);
     int64_t *dch;
     {
         int64_t hch[4 * kRegMaxChunks] = {};
@@ -572,8 +157,9 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     double *ellv = ufast ? nullptr : (double *)c->buf("er_reg_ellv").ensure(sizeof(double) * 8 * n);
     auto *ocol = (uint16_t *)c->buf("er_reg_ocol").ensure(sizeof(uint16_t) * (nov + 1));
     double *oval = ufast ? nullptr : (double *)c->buf("er_reg_oval").ensure(sizeof(double) * (nov + 1));
-    k_ell8_fill<<<grid_for(n, 256, 8192), 256, 0, s>>>((int32_t)n, T, dch, pad, lp, li, lv, optr, ell,
-                                                      ellv, ocol, oval);
+    k_ell8_fill<<<grid_for(n, 256, 8192), 256, 0, s>>>((int32_t)n, T, dch, pad, G,
+                                                      ufast ? (int32_t)zs + 2 : -1, lp, li, lv, optr,
+                                                      ell, ellv, ocol, oval);
     GS_HIP(hipGetLastError());
     double *pg = (double *)c->buf("er_reg_pg").ensure(sizeof(double) * (size_t)slots * ldn);
     RegArgs A{};
@@ -602,32 +188,10 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     A.ck = dch + 2 * kRegMaxChunks;
     A.cb = dch + 3 * kRegMaxChunks;
     A.prof = prof;
-    const int rsel = rneed <= 16 ? 16 : rneed <= 24 ? 24 : rneed <= 32 ? 32 : 44;
-#define GS_REG(G_, R_, U_)                                                                     \
-    do {                                                                                       \
-        GS_HIP(hipFuncSetAttribute((const void *)k_cg_regres<G_, R_, U_>,                      \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));    \
-        k_cg_regres<G_, R_, U_><<<(unsigned)slots, kRegThreads, dyn, s>>>(A);                 \
-    } while (0)
-#define GS_REG_R(G_, U_)                          \
-    do {                                          \
-        if (rsel == 16) GS_REG(G_, 16, U_);       \
-        else if (rsel == 24) GS_REG(G_, 24, U_);  \
-        else if (rsel == 32) GS_REG(G_, 32, U_);  \
-        else GS_REG(G_, 44, U_);                  \
-    } while (0)
-#define GS_REG_G(U_)                          \
-    do {                                      \
-        if (G == 1) GS_REG_R(1, U_);          \
-        else if (G == 2) GS_REG_R(2, U_);     \
-        else if (G == 4) GS_REG_R(4, U_);     \
-        else GS_REG_R(8, U_);                 \
-    } while (0)
-    if (ufast) GS_REG_G(true);
-    else GS_REG_G(false);
-#undef GS_REG_G
-#undef GS_REG_R
-#undef GS_REG
+    if (G == 1) regres_launch_g1(A, rsel, ufast, dyn, (unsigned)slots, s);
+    else if (G == 2) regres_launch_g2(A, rsel, ufast, dyn, (unsigned)slots, s);
+    else if (G == 4) regres_launch_g4(A, rsel, ufast, dyn, (unsigned)slots, s);
+    else regres_launch_g8(A, rsel, ufast, dyn, (unsigned)slots, s);
     GS_HIP(hipGetLastError());
 }
 
