@@ -26,10 +26,12 @@ __device__ __forceinline__ uint32_t p_code(int32_t c, int T, const int64_t *__re
                                           : 0x8000u | (uint32_t)c;
 }
 
-// diagonal slot index (2 tid + parity) of row c in k_cg_regres (G threads per chain):
+// diagonal slot index of row c: 2 tid + parity in k_cg_regres (dmul 2), tid in
+// k_cg_regwide (dmul 1), G threads per chain:
 // chain row s of chain (t, j) is slot s / G of thread g = s % G; a chunk's tail rows
 // belong to g = 0 with parity 0
-__device__ __forceinline__ int row_dslot(int32_t c, int T, const int64_t *__restrict__ tab, int G) {
+__device__ __forceinline__ int row_dslot(int32_t c, int T, const int64_t *__restrict__ tab, int G,
+                                         int dmul) {
     int t = 0;
     while (t + 1 < T && c >= tab[t + 1]) ++t;
     const int o = (int)(c - tab[t]), n32 = (int)(tab[kRegMaxChunks + t] & ~(int64_t)31);
@@ -37,13 +39,14 @@ __device__ __forceinline__ int row_dslot(int32_t c, int T, const int64_t *__rest
     const int j = in ? (o & 31) : o - n32, g = in ? (o >> 5) % G : 0;
     const int par = in ? ((o >> 5) / G) & 1 : 0;
     const int chain = t * 32 + j, CW = 64 / G;
-    return 2 * ((chain / CW) * 64 + (chain % CW) + CW * g) + par;
+    const int tid = (chain / CW) * 64 + (chain % CW) + CW * g;
+    return dmul == 2 ? 2 * tid + par : tid;
 }
 
 // dslot0 >= 0 (unit form): the diagonal entry's code is the owner thread's diagonal
 // slot dslot0 + tid instead of the row's p code
 __global__ void k_ell8_fill(int32_t n, int T, const int64_t *__restrict__ tab, uint32_t pad,
-                            int G, int32_t dslot0, const int64_t *__restrict__ lp,
+                            int G, int dmul, int32_t dslot0, const int64_t *__restrict__ lp,
                             const int32_t *__restrict__ li, const double *__restrict__ lv,
                             const int64_t *__restrict__ optr, uint4 *__restrict__ ell,
                             double *__restrict__ ellv, uint16_t *__restrict__ ocol,
@@ -51,7 +54,7 @@ __global__ void k_ell8_fill(int32_t n, int T, const int64_t *__restrict__ tab, u
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e0 = lp[i], len = lp[i + 1] - e0;
-        const uint32_t dcode = dslot0 >= 0 ? (uint32_t)(dslot0 + row_dslot((int32_t)i, T, tab, G)) : 0u;
+        const uint32_t dcode = dslot0 >= 0 ? (uint32_t)(dslot0 + row_dslot((int32_t)i, T, tab, G, dmul)) : 0u;
         auto code = [&](int64_t e) -> uint32_t {
             return (dslot0 >= 0 && li[e] == i) ? dcode : p_code(li[e], T, tab);
         };
@@ -80,12 +83,21 @@ static int reg_geometry(int NT, int T, const int64_t *len, int &G) {
     return (int)((smax + G - 1) / G);
 }
 
-// workgroup size and slots: 256 threads (one wave per SIMD, 512 registers per lane)
-// where the slots fit 88, else 512 threads (two waves per SIMD) with up to 44
+// workgroup size and slots: 512 threads (two waves per SIMD, k_cg_regwide) where the
+// slots fit 44, else 256 threads (one wave per SIMD, 512 registers per lane,
+// k_cg_regres) with up to 88.  GSPARSE_REG_NT=256 forces the one-wave form.
 static bool reg_pick(int64_t n, int T, const int64_t *len, int &NT, int &G, int &R) {
     if (n <= 0 || n >= 0x8000) return false;
     int g = 0;
-    const int r = reg_geometry(256, T, len, g);
+    const char *e = getenv("GSPARSE_REG_NT");
+    const bool narrow_only = e && atoi(e) == 256;
+    int r = narrow_only ? -1 : reg_geometry(512, T, len, g);
+    if (r >= 0 && r <= 44) {
+        NT = 512, G = g;
+        R = r <= 16 ? 16 : r <= 24 ? 24 : r <= 32 ? 32 : 44;
+        return true;
+    }
+    r = reg_geometry(256, T, len, g);
     if (r < 0 || r > 88) return false;
     NT = 256, G = g;
     R = r <= 24 ? 24 : r <= 48 ? 48 : r <= 64 ? 64 : 88;
@@ -95,6 +107,11 @@ static bool reg_pick(int64_t n, int T, const int64_t *len, int &NT, int &G, int 
 bool cg_regres_applies(int64_t n, int T, const int64_t *len) {
     int NT, G, R;
     return reg_pick(n, T, len, NT, G, R);
+}
+
+bool cg_regres_wide(int64_t n, int T, const int64_t *len) {
+    int NT = 0, G, R;
+    return reg_pick(n, T, len, NT, G, R) && NT == 512;
 }
 
 void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li, const double *lv,
@@ -117,11 +134,14 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     GS_HIP(hipMemcpyAsync(&nov, optr + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     GS_HIP(hipStreamSynchronize(s));
     // LDS: p (each chunk's LDS-resident prefix, in chunk order), the zero and scratch
-    // slots, 6 x 32 T doubles of chain sums / tail rows, the chunk table
+    // slots, (one-wave form) 2 diagonal slots per thread, 6 x 32 T doubles of chain
+    // sums / tail rows, the chunk table
     const int nch = 32 * T;
+    const bool ufast = unit && dcount;  // the unit kernels derive every diagonal from the entry count
+    const int dsl = NT == 256 ? 2 * NT : ufast ? NT : 0;
     const size_t lds_max = 160 * 1024;
     const int64_t cap =
-        (int64_t)((lds_max - (6 * (size_t)nch + 2 * kRegMaxChunks + 2 + 2 * NT) * 8) / 8);
+        (int64_t)((lds_max - (6 * (size_t)nch + 2 * kRegMaxChunks + 2 + dsl) * 8) / 8);
     // prefixes in proportion to the chunk lengths, whole wave-slots (32 G rows) when
     // they cannot all fit
     int64_t keep[kRegMaxChunks], lbase[kRegMaxChunks], tot = 0;
@@ -138,7 +158,7 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     }
     const uint32_t pad = (uint32_t)zs;  // the zero slot
     const size_t dyn =
-        sizeof(double) * ((size_t)zs + 2 + 2 * NT + 6 * (size_t)nch + 2 * kRegMaxChunks);
+        sizeof(double) * ((size_t)zs + 2 + dsl + 6 * (size_t)nch + 2 * kRegMaxChunks);
     int64_t *dch;
     {
         int64_t hch[4 * kRegMaxChunks] = {};
@@ -152,12 +172,10 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
         GS_HIP(hipMemcpy(dch, hch, sizeof(hch), hipMemcpyHostToDevice));
     }
     auto *ell = (uint4 *)c->buf("er_reg_ell").ensure(sizeof(uint4) * n);
-    // the unit kernel derives every diagonal from the entry count: other graphs carry weights
-    const bool ufast = unit && dcount;
     double *ellv = ufast ? nullptr : (double *)c->buf("er_reg_ellv").ensure(sizeof(double) * 8 * n);
     auto *ocol = (uint16_t *)c->buf("er_reg_ocol").ensure(sizeof(uint16_t) * (nov + 1));
     double *oval = ufast ? nullptr : (double *)c->buf("er_reg_oval").ensure(sizeof(double) * (nov + 1));
-    k_ell8_fill<<<grid_for(n, 256, 8192), 256, 0, s>>>((int32_t)n, T, dch, pad, G,
+    k_ell8_fill<<<grid_for(n, 256, 8192), 256, 0, s>>>((int32_t)n, T, dch, pad, G, NT == 256 ? 2 : 1,
                                                       ufast ? (int32_t)zs + 2 : -1, lp, li, lv, optr,
                                                       ell, ellv, ocol, oval);
     GS_HIP(hipGetLastError());
@@ -188,7 +206,12 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     A.ck = dch + 2 * kRegMaxChunks;
     A.cb = dch + 3 * kRegMaxChunks;
     A.prof = prof;
-    if (G == 1) regres_launch_g1(A, rsel, ufast, dyn, (unsigned)slots, s);
+    if (NT == 512) {
+        if (G == 1) regwide_launch_g1(A, rsel, ufast, dyn, (unsigned)slots, s);
+        else if (G == 2) regwide_launch_g2(A, rsel, ufast, dyn, (unsigned)slots, s);
+        else if (G == 4) regwide_launch_g4(A, rsel, ufast, dyn, (unsigned)slots, s);
+        else regwide_launch_g8(A, rsel, ufast, dyn, (unsigned)slots, s);
+    } else if (G == 1) regres_launch_g1(A, rsel, ufast, dyn, (unsigned)slots, s);
     else if (G == 2) regres_launch_g2(A, rsel, ufast, dyn, (unsigned)slots, s);
     else if (G == 4) regres_launch_g4(A, rsel, ufast, dyn, (unsigned)slots, s);
     else regres_launch_g8(A, rsel, ufast, dyn, (unsigned)slots, s);

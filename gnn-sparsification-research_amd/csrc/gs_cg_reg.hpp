@@ -564,6 +564,15 @@ GS_REGRES_LAUNCH_DECL(2)
 GS_REGRES_LAUNCH_DECL(4)
 GS_REGRES_LAUNCH_DECL(8)
 #undef GS_REGRES_LAUNCH_DECL
+// one launch of k_cg_regwide<G, R, UNIT> (512 threads, gs_cg_wide.hpp)
+#define GS_REGWIDE_LAUNCH_DECL(G_)                                                            \
+    void regwide_launch_g##G_(const RegArgs &A, int R, bool unit, size_t dyn, unsigned slots, \
+                              hipStream_t s);
+GS_REGWIDE_LAUNCH_DECL(1)
+GS_REGWIDE_LAUNCH_DECL(2)
+GS_REGWIDE_LAUNCH_DECL(4)
+GS_REGWIDE_LAUNCH_DECL(8)
+#undef GS_REGWIDE_LAUNCH_DECL
 
 // one launch of the kernel: R row slots (24 / 48 / 64 / 88), unit or weighted form
 #define GS_REGRES_LAUNCH_DEF(G_)                                                              \

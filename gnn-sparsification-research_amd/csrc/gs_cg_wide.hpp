@@ -1,0 +1,486 @@
+// gs_cg_wide.hpp -- the 512-thread form of the register-resident CG (ApproxER mode
+// 5; design notes in gs_cg_reg.hpp).  Two waves per SIMD, 256 registers per lane:
+// r and x of up to 44 row slots per thread, the allocator's own VGPR / AGPR split.
+// The second wave on each SIMD hides the LDS and fp64 latencies that the
+// one-wave form (k_cg_regres, up to 88 slots) must pipeline by hand, so this
+// form runs wherever the slots fit 44 (Roman-empire: 8 chunks, 2 threads per
+// chain, 44 slots); k_cg_regres takes the larger graphs.  Instantiated per G in
+// gs_cg_reg_g{1,2,4,8}.hip.
+#pragma once
+#include "gs_cg_reg.hpp"
+
+namespace gs {
+
+// byte address (p code * 8) of the low / high 16-bit p code of an ELL word: one SDWA
+// shift (word select + shift) instead of an extract and a shift
+template <int HI>
+__device__ __forceinline__ uint32_t wide_code_addr(uint32_t w) {
+    uint32_t a;
+    if (HI)
+        asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+            : "=v"(a) : "v"(w));
+    else
+        asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+            : "=v"(a) : "v"(w));
+    return a;
+}
+
+// v of lane K of each quad (DPP quad_perm broadcast, both dwords)
+template <int K>
+__device__ __forceinline__ double wide_quad_bcast(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)b, K * 0x55, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), K * 0x55, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// v of lane ln (wave-uniform ln), as a scalar
+__device__ __forceinline__ double wide_readlane(double v, int ln) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, ln);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), ln);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// G threads per chain (power of two), R row slots per thread, UNIT: every
+// off-diagonal weight is -1.0 and every diagonal one fl((entries - 1) + 1e-6) (no
+// weights loaded; q_i folds -p_j and dg * p_i); else the ELL carries the weights
+template <int G, int R, bool UNIT>
+__global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
+    constexpr int CW = 64 / G;  // chains per wave
+    extern __shared__ double lds[];
+    const int T = A.T, nch = 32 * T;
+    // LDS: p at offset 0 (a gather's address is its code * 8), the zero and scratch
+    // slots, (unit form) one diagonal slot per thread, then chain sums, tail rows and
+    // the chunk table
+    double *sp = lds;
+    double *acc_pq = lds + A.zslot + 2 + (UNIT ? kRegThreads : 0), *acc_rr = acc_pq + nch;
+    double *side_p = acc_pq + 2 * nch, *side_q = acc_pq + 3 * nch, *side_r = acc_pq + 4 * nch;
+    double *side_x = acc_pq + 5 * nch;  // tail rows' r lives in side_r, x here
+    // [4][kRegMaxChunks]: starts, lengths, LDS-resident prefix, its LDS base
+    int *s_ch = reinterpret_cast<int *>(acc_pq + 6 * nch);
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (tid < T) {
+        s_ch[tid] = (int)A.ca[tid];
+        s_ch[kRegMaxChunks + tid] = (int)A.cl[tid];
+        s_ch[2 * kRegMaxChunks + tid] = (int)A.ck[tid];
+        s_ch[3 * kRegMaxChunks + tid] = (int)A.cb[tid];
+    }
+    __syncthreads();
+    const int jj = lane % CW, g = lane / CW;
+    const int chain = (tid >> 6) * CW + jj;
+    const bool live = chain < nch;
+    const int t = live ? chain >> 5 : 0, j = chain & 31;
+    const int L = s_ch[kRegMaxChunks + t];
+    const int n32 = L & ~31;
+    const int S = live ? n32 >> 5 : -1;  // chain rows; row s == S is a tail row when j < tl
+    const int tl = L - n32;
+    int base = s_ch[t] + j + 32 * g;  // row of slot u: base + 32 G u
+    // register slots u < uc hold chain rows; the chunk's tail row s == S (j < tl) is
+    // kept by the g == 0 lane with its r and x in LDS (side_r / side_x)
+    int uc = S > g ? (S - g + G - 1) / G : 0;
+    const bool tail = live && g == 0 && j < tl;
+    const int trow = s_ch[t] + n32 + j;
+    const int tix = t * 32 + j;
+    int Sv = S;
+    // Re-derive the per-slot rows and conditions inside every phase: left loop-
+    // invariant, the compiler hoists all R of them out of the iteration loop and
+    // keeps them live (hundreds of SGPRs/VGPRs, spilled to scratch).
+    auto launder = [&]() { asm volatile("" : "+v"(base), "+v"(uc), "+v"(Sv)); };
+    const int ca_t = s_ch[t], keep_t = s_ch[2 * kRegMaxChunks + t], lbase_t = s_ch[3 * kRegMaxChunks + t];
+    const int zslot = A.zslot;  // LDS slot holding 0.0 (the ELL padding code)
+    // explicit address spaces: a select between an LDS and a global pointer would
+    // become one (slow) flat load
+    typedef __attribute__((address_space(3))) double lds_f64;
+    typedef __attribute__((address_space(3))) char lds_u8;
+    lds_f64 *spl = (lds_f64 *)sp;
+    double *pgw = A.pg + (int64_t)blockIdx.x * A.ldn;
+    // rows of p outside LDS: raw buffer, offsets past its size read 0 / drop the store
+    const __amdgpu_buffer_rsrc_t prs =
+        __builtin_amdgcn_make_buffer_rsrc(pgw, 0, (int)(A.ldn * 8), 0x00020000);
+    constexpr int kOob = (int)0x80000000;
+    if (tid == 0) spl[zslot] = 0.0;
+
+    // p of a row lives at its code: an LDS slot (< 0x8000) or 0x8000 | row (global);
+    // code_of takes a row of this lane's chunk
+    auto code_of = [&](int row) {
+        const int o = row - ca_t;
+        return o < keep_t ? lbase_t + o : 0x8000 | row;
+    };
+    // LDS access always; the global one only under a wave-uniform branch (a wave's
+    // rows of one slot are 32 G consecutive rows of a chunk, mostly all LDS-resident)
+    auto ldc = [&](int cd) -> double {
+        double v = spl[cd < 0x8000 ? cd : zslot];
+        if (__builtin_amdgcn_ballot_w64(cd >= 0x8000)) {
+            const double vg = __builtin_bit_cast(
+                double, __builtin_amdgcn_raw_buffer_load_b64(prs, cd < 0x8000 ? kOob : (cd & 0x7fff) * 8, 0, 0));
+            v = cd < 0x8000 ? v : vg;
+        }
+        return v;
+    };
+    auto stc = [&](int cd, double v) {
+        spl[cd < 0x8000 ? cd : zslot + 1] = v;  // zslot + 1: a scratch slot
+        if (__builtin_amdgcn_ballot_w64(cd >= 0x8000))
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), prs,
+                cd < 0x8000 ? kOob : (cd & 0x7fff) * 8, 0, 0);
+    };
+    auto valid = [&](int u) { return u < uc; };
+    const uint32_t pad2 = (uint32_t)zslot | ((uint32_t)zslot << 16);
+    auto ell_row = [&](int u) -> uint4 {
+        return valid(u) ? A.ell[base + 32 * G * u] : make_uint4(pad2, pad2, pad2, pad2);
+    };
+    auto len_row = [&](int u) -> int { return valid(u) ? (int)A.rlen[base + 32 * G * u] : 0; };
+    auto rowof = [&](int u) { return base + 32 * G * u; };
+
+    // q_i = (L_reg p)_i, SciPy csr_matvec: fold from 0.0 in ascending column, products
+    // rounded; pown receives p_i.  Entries are p codes.  Unit form: off-diagonal
+    // products are -p_j exactly (-1.0 * x == -x) and the diagonal one td = fl(dg * p_i);
+    // the diagonal entry's code is this thread's diagonal slot, which receives -td
+    // before the gathers (a wave's LDS operations complete in order), so every entry
+    // folds as acc - v: acc - (-td) == acc + td and acc - p_j == acc + (-p_j) bit for bit.
+    // Padding entries gather the zero slot: +-0.0 terms, and acc + (+-0.0) == acc bit
+    // for bit (acc starts at +0.0 and is never -0.0).  Codes of global rows read past
+    // the LDS (no fault; the value is replaced under one wave-uniform branch), so the
+    // slot issues no memory load whose result it waits for -- the ELL rows prefetched
+    // for the next slots stay in flight.
+    const int dslot = zslot + 2 + tid;
+    auto spmv = [&](int row, const uint4 e, int len, double &pown) -> double {
+        const int self = code_of(row);
+        const uint32_t w4[4] = {e.x, e.y, e.z, e.w};
+        uint32_t ad[8];  // LDS byte addresses; global codes land past the LDS (read as 0)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ad[k] = (k & 1) ? wide_code_addr<1>(w4[k >> 1]) : wide_code_addr<0>(w4[k >> 1]);
+        double td = 0.0;
+        if (UNIT) {
+            pown = ldc(self);
+            const double dg = (double)(len - 1) + 1e-6;  // UNIT: L_reg_ii == fl((entries - 1) + 1e-6)
+            td = dg * pown;
+            spl[dslot] = -td;
+        }
+        double pv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) pv[k] = *(lds_f64 *)((lds_u8 *)spl + ad[k]);
+        if (!UNIT) pown = spl[self];
+        const bool anyg = ((w4[0] | w4[1] | w4[2] | w4[3]) & 0x80008000u) != 0 || (!UNIT && self >= 0x8000);
+        if (__builtin_amdgcn_ballot_w64(anyg)) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const bool gk = ad[k] >= 0x8000u * 8;
+                const double vg = __builtin_bit_cast(
+                    double, __builtin_amdgcn_raw_buffer_load_b64(prs, gk ? (int)(ad[k] & 0x3fff8u) : kOob, 0, 0));
+                pv[k] = gk ? vg : pv[k];
+            }
+            if (!UNIT) pown = ldc(self);
+        }
+        double acc = 0.0;
+        if (UNIT) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc = acc - pv[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const double prod = A.ellv[(int64_t)row * 8 + k] * pv[k];
+                acc = acc + prod;
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(len > 8)) {  // rows longer than 8 entries: ocol / oval
+            const int64_t o0 = len > 8 ? A.optr[row] : 0, o1 = len > 8 ? A.optr[row + 1] : 0;
+            for (int64_t q = o0; q < o1; ++q) {
+                const int cc = (int)A.ocol[q];
+                const double pc = ldc(cc);
+                if (UNIT) acc = acc - pc;  // the diagonal's code is the diagonal slot
+                else acc = acc + A.oval[q] * pc;
+            }
+        }
+        return acc;
+    };
+
+    // lanes 0..31 receive v of lanes 32..63 (v_permlane32_swap)
+    auto upper_half = [](double v) -> double {
+        const uint64_t b = (uint64_t)__double_as_longlong(v);
+        const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false);
+        const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+        return __longlong_as_double((long long)(((uint64_t)hi[1] << 32) | lo[1]));
+    };
+    // one step of every chain: rows s = G u + gg (gg < G) in order, folded by the g = 0 lane
+    auto chain_step = [&](double &acc, double av, double bv, int u, bool same = false) {
+        double as[G], bs[G];
+        as[0] = av;  // the folding lane's own row (g = 0)
+        bs[0] = bv;
+        if (G == 2) {  // partner = lane + 32: one permlane swap per dword, no LDS
+            as[G - 1] = upper_half(av);
+            bs[G - 1] = same ? as[G - 1] : upper_half(bv);  // same: bv is av
+        } else {
+#pragma unroll
+            for (int gg = 1; gg < G; ++gg) {
+                as[gg] = __shfl(av, jj + CW * gg, 64);
+                bs[gg] = __shfl(bv, jj + CW * gg, 64);
+            }
+        }
+#pragma unroll
+        for (int gg = 0; gg < G; ++gg)
+            if (G * u + gg < Sv) acc = __builtin_fma(as[gg], bs[gg], acc);
+        // fold now: deferred, every slot's shuffled operands would stay live to the end
+        asm volatile("" : "+v"(acc));
+    };
+
+    // OpenBLAS finish of one dot (every wave computes it; lane = chunk)
+    // lanes 4 t + l (t < T, l < 4) fold c4[l] of chunk t with all their LDS loads in
+    // flight; lane 4 t collects its quad's four (DPP) and adds the chunk's FMA tail; the
+    // chunks are summed in order from scalar reads (v_readlane), so the result is
+    // wave-uniform without a broadcast
+    auto finish = [&](const double *acc32all, const double *xa_all, const double *xb_all) -> double {
+        const int tq = lane >> 2, l = lane & 3;
+        const bool lv = tq < T;
+        const int Lt = s_ch[kRegMaxChunks + (lv ? tq : 0)];
+        const int n1 = Lt & ~15, n32t = n1 & ~31;
+        const double *a32 = acc32all + tq * 32;  // dereferenced only when lv
+        const double *xa = xa_all + tq * 32, *xb = xb_all + tq * 32;
+        double cl = 0.0;
+        if (lv && n1) {
+            // b[4q + l] = acc[8q + l] + acc[8q + 4 + l] (+ the 16-block row 4q + l),
+            // c4[l] = ((b[l] + b[4 + l]) + b[8 + l]) + b[12 + l]
+            const bool blk = n1 > n32t;
+            double av[4], bv[4], pa[4], pb[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                av[q] = a32[8 * q + l];
+                bv[q] = a32[8 * q + 4 + l];
+                pa[q] = blk ? xa[4 * q + l] : 0.0;
+                pb[q] = blk ? xb[4 * q + l] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                double b = av[q] + bv[q];
+                if (blk) b = __builtin_fma(pa[q], pb[q], b);
+                cl = q == 0 ? b : cl + b;
+            }
+        }
+        const double c0 = wide_quad_bcast<0>(cl), c1 = wide_quad_bcast<1>(cl);
+        const double c2 = wide_quad_bcast<2>(cl), c3 = wide_quad_bcast<3>(cl);
+        double dot = n1 ? (c0 + c2) + (c1 + c3) : 0.0;
+        if (lv && l == 0) {
+            const int nt = Lt - n1, ib = n1 - n32t;  // tail rows (< 16) after the 16-block
+            for (int i0 = 0; i0 < nt; i0 += 4) {
+                double ta[4], tb[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    ta[i] = i0 + i < nt ? xa[ib + i0 + i] : 0.0;
+                    tb[i] = i0 + i < nt ? xb[ib + i0 + i] : 0.0;
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (i0 + i < nt) dot = __builtin_fma(tb[i], ta[i], dot);
+            }
+        }
+        if (T == 1) return wide_readlane(dot, 0);
+        double total = 0.0;
+        for (int tt = 0; tt < T; ++tt) total = total + wide_readlane(dot, 4 * tt);
+        return total;
+    };
+
+    long long tp[5] = {0, 0, 0, 0, 0};
+    long long tmark = wall_clock64();
+    auto lap = [&](int ph) {
+        const long long tn = wall_clock64();
+        tp[ph] += tn - tmark;
+        tmark = tn;
+    };
+
+    for (int64_t ci = blockIdx.x; ci < A.ncols; ci += gridDim.x) {
+        const int64_t c = A.col0 + ci;
+        double r[R], x[R];
+        // r = b.copy(); rho_0 = b.b
+        {
+            launder();
+            double acc = 0.0;
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                x[u] = 0.0;
+                r[u] = valid(u) ? A.Rr[(int64_t)rowof(u) * A.ld + c] : 0.0;
+                chain_step(acc, r[u], r[u], u, true);
+            }
+            if (g == 0 && live) acc_rr[chain] = acc;
+            if (tail) {
+                side_r[tix] = A.Rr[(int64_t)trow * A.ld + c];
+                side_x[tix] = 0.0;
+            }
+        }
+        __syncthreads();
+        double rr = finish(acc_rr, side_r, side_r);
+        const double bn = __builtin_sqrt(rr);
+        const double atol = A.rtol * bn;  // max(atol=0, rtol*bnrm2)
+        int32_t done = 0;
+        double rho_prev = 0.0, alpha_prev = 0.0;
+        const bool act = !(bn == 0.0) && !(__builtin_sqrt(rr) < atol);
+        for (int32_t it = 0; act && it < A.maxiter; ++it) {
+            if (it > 0 && __builtin_sqrt(rr) < atol) break;  // loop-top test
+            const double rho_cur = rr;
+            const double beta = it > 0 ? rho_cur / rho_prev : 0.0;
+            lap(4);
+            // p = beta p + r (two roundings); x += alpha_{it-1} p_{it-1} rides along
+            launder();
+            if (it == 0) {
+#pragma unroll
+                for (int u = 0; u < R; ++u)
+                    if (valid(u)) stc(code_of(rowof(u)), r[u]);
+            } else {
+                double pb4[R];  // p_old, kPre slots ahead (each slot reads and writes only its row)
+#pragma unroll
+                for (int u = 0; u < kPre && u < R; ++u) pb4[u] = valid(u) ? ldc(code_of(rowof(u))) : 0.0;
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    if (u + kPre < R) pb4[u + kPre] = valid(u + kPre) ? ldc(code_of(rowof(u + kPre))) : 0.0;
+                    if (valid(u)) {
+                        const double po = pb4[u];
+                        const double t1 = alpha_prev * po;
+                        x[u] = x[u] + t1;
+                        const double pb = po * beta;
+                        stc(code_of(rowof(u)), pb + r[u]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            if (tail) {
+                if (it == 0) {
+                    stc(code_of(trow), side_r[tix]);
+                } else {
+                    const double po = ldc(code_of(trow));
+                    const double t1 = alpha_prev * po;
+                    side_x[tix] = side_x[tix] + t1;
+                    const double pb = po * beta;
+                    stc(code_of(trow), pb + side_r[tix]);
+                }
+            }
+            __syncthreads();
+            lap(0);
+            // q = L_reg p and the chains of p.q
+            {
+                launder();
+                double acc = 0.0;
+                uint4 eb[R];  // ELL rows and lengths, kPre slots ahead
+                int lb[R];
+#pragma unroll
+                for (int u = 0; u < kPre && u < R; ++u) {
+                    eb[u] = ell_row(u);
+                    lb[u] = len_row(u);
+                }
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    if (u + kPre < R) {
+                        eb[u + kPre] = ell_row(u + kPre);
+                        lb[u + kPre] = len_row(u + kPre);
+                    }
+                    double pv = 0.0, qv = 0.0;
+                    if (valid(u)) qv = spmv(rowof(u), eb[u], lb[u], pv);
+                    chain_step(acc, pv, qv, u);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (g == 0 && live) acc_pq[chain] = acc;
+                if (tail) {
+                    double pt;
+                    side_q[tix] = spmv(trow, A.ell[trow], (int)A.rlen[trow], pt);
+                    side_p[tix] = pt;
+                }
+            }
+            __syncthreads();
+            lap(1);
+            const double pq = finish(acc_pq, side_p, side_q);
+            const double alpha = rho_cur / pq;
+            lap(2);
+            // r -= alpha q (q recomputed), chains of r.r
+            {
+                launder();
+                double acc = 0.0;
+                uint4 eb[R];
+                int lb[R];
+#pragma unroll
+                for (int u = 0; u < kPre && u < R; ++u) {
+                    eb[u] = ell_row(u);
+                    lb[u] = len_row(u);
+                }
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    if (u + kPre < R) {
+                        eb[u + kPre] = ell_row(u + kPre);
+                        lb[u + kPre] = len_row(u + kPre);
+                    }
+                    if (valid(u)) {
+                        double pu;
+                        const double t2 = alpha * spmv(rowof(u), eb[u], lb[u], pu);
+                        r[u] = r[u] - t2;
+                    }
+                    chain_step(acc, r[u], r[u], u, true);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (g == 0 && live) acc_rr[chain] = acc;
+                if (tail) {
+                    double pt;
+                    const double t2 = alpha * spmv(trow, A.ell[trow], (int)A.rlen[trow], pt);
+                    side_r[tix] = side_r[tix] - t2;
+                }
+            }
+            __syncthreads();
+            lap(3);
+            rr = finish(acc_rr, side_r, side_r);
+            rho_prev = rho_cur;
+            alpha_prev = alpha;
+            done = it + 1;
+        }
+        // x: b (||b|| == 0), 0 (no iteration), or the last pending update
+        launder();
+        double *xo = A.Xc + ci * A.ldn;
+#pragma unroll
+        for (int u = 0; u < R; ++u)
+            if (valid(u)) {
+                const int row = rowof(u);
+                double v;
+                if (bn == 0.0) v = r[u];
+                else if (done == 0) v = 0.0;
+                else {
+                    const double t1 = alpha_prev * ldc(code_of(row));
+                    v = (done > 1 ? x[u] : 0.0) + t1;
+                }
+                xo[row] = v;
+            }
+        if (tail) {
+            double v;
+            if (bn == 0.0) v = side_r[tix];
+            else if (done == 0) v = 0.0;
+            else {
+                const double t1 = alpha_prev * ldc(code_of(trow));
+                v = (done > 1 ? side_x[tix] : 0.0) + t1;
+            }
+            xo[trow] = v;
+        }
+        if (tid == 0) A.iters[c] = done;
+        __syncthreads();  // the next column's b.b chains reuse acc_rr / side_r
+    }
+    if (A.prof && blockIdx.x == 0 && tid == 0)
+        for (int i = 0; i < 5; ++i) A.prof[i] = tp[i];
+}
+
+// one launch: R row slots (16 / 24 / 32 / 44), unit or weighted form
+#define GS_REGWIDE_LAUNCH_DEF(G_)                                                             \
+    void regwide_launch_g##G_(const RegArgs &A, int R, bool unit, size_t dyn, unsigned slots, \
+                              hipStream_t s) {                                                \
+        auto go = [&](auto kern) {                                                            \
+            GS_HIP(hipFuncSetAttribute((const void *)kern,                                    \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn)); \
+            kern<<<slots, kRegThreads, dyn, s>>>(A);                                          \
+        };                                                                                    \
+        if (unit) {                                                                           \
+            if (R == 16) go(k_cg_regwide<G_, 16, true>);                                      \
+            else if (R == 24) go(k_cg_regwide<G_, 24, true>);                                 \
+            else if (R == 32) go(k_cg_regwide<G_, 32, true>);                                 \
+            else go(k_cg_regwide<G_, 44, true>);                                              \
+        } else {                                                                              \
+            if (R == 16) go(k_cg_regwide<G_, 16, false>);                                     \
+            else if (R == 24) go(k_cg_regwide<G_, 24, false>);                                \
+            else if (R == 32) go(k_cg_regwide<G_, 32, false>);                                \
+            else go(k_cg_regwide<G_, 44, false>);                                             \
+        }                                                                                     \
+    }
+
+}  // namespace gs

@@ -1756,10 +1756,12 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         // Roman size, 2,674 columns: 0.51 s vs 0.53 s for mode 0; k/8 columns ~0.09 s vs 0.12 s.
         const bool resident = n > 10000 && n <= 24576 && ch.count >= 4 &&
                               er.lnnz <= kStoreQRowLen * n;
-        // register-resident solver (5): opt-in (GSPARSE_CG_MODE=5) until it beats mode 4
-        // at the configs[1] size
+        // register-resident solver (5) where its 512-thread form applies (Roman size:
+        // 55.7 vs 76.4 us per column-iteration for mode 4); its
+        // 256-thread form (more rows per thread) is no faster than mode 4: opt-in
         const bool regres = cg_regres_applies(n, ch.count, ch.len);
-        int mode = resident && regres && getenv("GSPARSE_CG_REGRES") ? 5
+        const bool regwide = cg_regres_wide(n, ch.count, ch.len);
+        int mode = resident && regwide                        ? 5
                    : resident                                 ? 4
                    : (n > 0 && er.lnnz > kStoreQRowLen * n) ? 3
                    : ncols >= 2048                          ? 0

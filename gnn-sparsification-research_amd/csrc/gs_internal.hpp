@@ -178,6 +178,7 @@ void ensure_transpose(gs_ctx *c);
 // chunks (lengths len[t]) fit its thread geometry; solves columns [col0, col0+ncols)
 // of L_reg (CSR lp/li/lv) into Xc (column-major, ldn per column)
 bool cg_regres_applies(int64_t n, int T, const int64_t *len);
+bool cg_regres_wide(int64_t n, int T, const int64_t *len);  // its 512-thread form applies
 void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li, const double *lv,
                      int unit, int dcount, const double *diag, const double *Rr, int64_t ld,
                      int64_t col0, int64_t ncols, int32_t maxiter, double rtol, int T,
