@@ -48,7 +48,7 @@ FP64_MFMA_PEAK_TFS = 78.6
 
 # profiler name -> kernel symbol prefix in the rocprofv3 summaries; "jaccard"
 # is a pipeline of kernels (plan, light, hash classes, bitmap), summed per call
-PMC_KERNEL = {"cg_res": "gs::k_cg_resident<", "cg_pq": "gs::k_cg_pq<false", "cg_upd": "gs::k_cg_upd<",
+PMC_KERNEL = {"cg_res": "gs::k_cg_resident<", "cg_reg": "gs::k_cg_reg", "cg_pq": "gs::k_cg_pq<false", "cg_upd": "gs::k_cg_upd<",
               "jaccard": "gs::k_jac_", "metric_backbone": "gs::k_bb_",
               "cg_p": "gs::k_cg_p", "cg_spmv": "gs::k_spmv<"}
 
@@ -700,8 +700,9 @@ def bench_scorers(args, world, rank, local_rank, dev, dist):
 
     per = {"jaccard": roof(["jaccard"], b_j), "adamic_adar": roof(["adamic_adar"], b_aa),
            "feature_cosine": roof(["featcos_normalise", "featcos_edges"], b_f)}
-    p = prof.get("cg_res") or max(prof.values(), key=lambda v: v["ms"])
-    name = "cg_res" if "cg_res" in prof else max(prof, key=lambda kk: prof[kk]["ms"])
+    name = next((kk for kk in ("cg_reg", "cg_res") if kk in prof), None) or max(
+        prof, key=lambda kk: prof[kk]["ms"])
+    p = prof[name]
     avg_ms = p["ms"] / p["launches"]
     achieved = p["bytes"] / p["launches"] / (avg_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(name, "roman") if world == 1 else (None, None)

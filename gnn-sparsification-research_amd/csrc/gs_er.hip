@@ -1960,7 +1960,7 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
 #undef GS_RES
             }
             GS_HIP(hipGetLastError());
-            prof_end(c, t0, "cg_res", 0.0);
+            prof_end(c, t0, mode == 5 ? "cg_reg" : "cg_res", 0.0);
             const bool prof_rec = c->profiling && !c->pending.empty();
             if (n)
                 k_cols_to_rows<<<dim3((unsigned)((n + 31) / 32), (unsigned)((ncols + 31) / 32)), 256, 0,
