@@ -82,23 +82,49 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     const bool tail = live && g == 0 && j < tl;
     const int trow = s_ch[t] + n32 + j;
     const int tix = t * 32 + j;
-    int Sv = S;
     // Re-derive the per-slot rows and conditions inside every phase: left loop-
     // invariant, the compiler hoists all R of them out of the iteration loop and
     // keeps them live (hundreds of SGPRs/VGPRs, spilled to scratch).
-    auto launder = [&]() { asm volatile("" : "+v"(base), "+v"(uc), "+v"(Sv)); };
+    int ulds = 0;  // set below
+    auto launder = [&]() { asm volatile("" : "+v"(base), "+v"(uc), "+s"(ulds)); };
     const int ca_t = s_ch[t], keep_t = s_ch[2 * kRegMaxChunks + t], lbase_t = s_ch[3 * kRegMaxChunks + t];
+    // slots u < ulds hold LDS-resident rows in every lane of the wave (a slot's rows are
+    // 32 G consecutive rows of one chunk per lane group and the prefixes are whole
+    // multiples of 32 G, so this is the wave's common prefix): their p lives at the
+    // byte address lds0 + 256 G u, an immediate offset -- no per-slot code, compare
+    // or select, and no global fix-up branch
+    {
+        int uk = R;  // lanes without chain rows never limit it
+        if (live) {
+            const int o0 = base - ca_t;
+            uk = keep_t > o0 ? (keep_t - o0 + 32 * G - 1) / (32 * G) : 0;
+        }
+        for (int off = 32; off >= 1; off >>= 1) uk = min(uk, __shfl_xor(uk, off, 64));
+        ulds = __builtin_amdgcn_readfirstlane(uk);
+    }
+    auto lds0 = [&]() -> uint32_t { return (uint32_t)(lbase_t + base - ca_t) * 8u; };
     const int zslot = A.zslot;  // LDS slot holding 0.0 (the ELL padding code)
     // explicit address spaces: a select between an LDS and a global pointer would
     // become one (slow) flat load
     typedef __attribute__((address_space(3))) double lds_f64;
-    typedef __attribute__((address_space(3))) char lds_u8;
+    auto lds_at = [](uint32_t a) -> double { return *(lds_f64 *)(uintptr_t)a; };
+    auto lds_put = [](uint32_t a, double v) { *(lds_f64 *)(uintptr_t)a = v; };
     lds_f64 *spl = (lds_f64 *)sp;
     double *pgw = A.pg + (int64_t)blockIdx.x * A.ldn;
     // rows of p outside LDS: raw buffer, offsets past its size read 0 / drop the store
     const __amdgpu_buffer_rsrc_t prs =
         __builtin_amdgcn_make_buffer_rsrc(pgw, 0, (int)(A.ldn * 8), 0x00020000);
     constexpr int kOob = (int)0x80000000;
+    // s_waitcnt vmcnt(0) inside a branch that loads p from the global slot: the waitcnt
+    // pass then sees no pending load at the join, and the ELL rows prefetched for the
+    // next slots stay in flight (otherwise every slot waits for them: vmcnt(0))
+    auto vm_drain = [] { __builtin_amdgcn_s_waitcnt(0x0f70); };
+    // ELL rows and entry counts: raw buffers (row offset in a VGPR, the slot's 32 G u
+    // rows as a scalar offset; rows past n read 0 and belong to no valid slot)
+    const __amdgpu_buffer_rsrc_t ers =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A.ell, 0, (int)(A.n * 16), 0x00020000);
+    const __amdgpu_buffer_rsrc_t lrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A.rlen, 0, (int)(A.n * 2), 0x00020000);
     if (tid == 0) spl[zslot] = 0.0;
 
     // p of a row lives at its code: an LDS slot (< 0x8000) or 0x8000 | row (global);
@@ -115,6 +141,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             const double vg = __builtin_bit_cast(
                 double, __builtin_amdgcn_raw_buffer_load_b64(prs, cd < 0x8000 ? kOob : (cd & 0x7fff) * 8, 0, 0));
             v = cd < 0x8000 ? v : vg;
+            vm_drain();
         }
         return v;
     };
@@ -126,11 +153,13 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                 cd < 0x8000 ? kOob : (cd & 0x7fff) * 8, 0, 0);
     };
     auto valid = [&](int u) { return u < uc; };
-    const uint32_t pad2 = (uint32_t)zslot | ((uint32_t)zslot << 16);
     auto ell_row = [&](int u) -> uint4 {
-        return valid(u) ? A.ell[base + 32 * G * u] : make_uint4(pad2, pad2, pad2, pad2);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(ers, base * 16, 512 * G * u, 0);
+        return make_uint4(v[0], v[1], v[2], v[3]);
     };
-    auto len_row = [&](int u) -> int { return valid(u) ? (int)A.rlen[base + 32 * G * u] : 0; };
+    auto len_row = [&](int u) -> int {
+        return (int)__builtin_amdgcn_raw_buffer_load_b16(lrs, base * 2, 64 * G * u, 0);
+    };
     auto rowof = [&](int u) { return base + 32 * G * u; };
 
     // q_i = (L_reg p)_i, SciPy csr_matvec: fold from 0.0 in ascending column, products
@@ -145,24 +174,26 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     // slot issues no memory load whose result it waits for -- the ELL rows prefetched
     // for the next slots stay in flight.
     const int dslot = zslot + 2 + tid;
-    auto spmv = [&](int row, const uint4 e, int len, double &pown) -> double {
-        const int self = code_of(row);
+    // u >= 0: register slot u (LDS fast path when u < ulds); u < 0: a tail row
+    auto spmv = [&](int row, const uint4 e, int len, double &pown, int u) -> double {
+        const bool fast = u >= 0 && u < ulds;  // wave-uniform
+        const int self = fast ? 0 : code_of(row);
         const uint32_t w4[4] = {e.x, e.y, e.z, e.w};
         uint32_t ad[8];  // LDS byte addresses; global codes land past the LDS (read as 0)
 #pragma unroll
         for (int k = 0; k < 8; ++k) ad[k] = (k & 1) ? wide_code_addr<1>(w4[k >> 1]) : wide_code_addr<0>(w4[k >> 1]);
         double td = 0.0;
         if (UNIT) {
-            pown = ldc(self);
+            pown = fast ? lds_at(lds0() + 256u * G * u) : ldc(self);
             const double dg = (double)(len - 1) + 1e-6;  // UNIT: L_reg_ii == fl((entries - 1) + 1e-6)
             td = dg * pown;
             spl[dslot] = -td;
         }
         double pv[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) pv[k] = *(lds_f64 *)((lds_u8 *)spl + ad[k]);
-        if (!UNIT) pown = spl[self];
-        const bool anyg = ((w4[0] | w4[1] | w4[2] | w4[3]) & 0x80008000u) != 0 || (!UNIT && self >= 0x8000);
+        for (int k = 0; k < 8; ++k) pv[k] = lds_at(ad[k]);
+        if (!UNIT) pown = fast ? lds_at(lds0() + 256u * G * u) : spl[self];
+        const bool anyg = ((w4[0] | w4[1] | w4[2] | w4[3]) & 0x80008000u) != 0 || (!UNIT && !fast && self >= 0x8000);
         if (__builtin_amdgcn_ballot_w64(anyg)) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
@@ -171,7 +202,8 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                     double, __builtin_amdgcn_raw_buffer_load_b64(prs, gk ? (int)(ad[k] & 0x3fff8u) : kOob, 0, 0));
                 pv[k] = gk ? vg : pv[k];
             }
-            if (!UNIT) pown = ldc(self);
+            if (!UNIT && !fast) pown = ldc(self);
+            vm_drain();
         }
         double acc = 0.0;
         if (UNIT) {
@@ -192,6 +224,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                 if (UNIT) acc = acc - pc;  // the diagonal's code is the diagonal slot
                 else acc = acc + A.oval[q] * pc;
             }
+            vm_drain();
         }
         return acc;
     };
@@ -218,9 +251,10 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                 bs[gg] = __shfl(bv, jj + CW * gg, 64);
             }
         }
+        // rows past the chain's end hold exact zeros (unset p / q, r of invalid slots):
+        // fma(0, 0, acc) == acc, acc never being -0.0 -- no per-row test
 #pragma unroll
-        for (int gg = 0; gg < G; ++gg)
-            if (G * u + gg < Sv) acc = __builtin_fma(as[gg], bs[gg], acc);
+        for (int gg = 0; gg < G; ++gg) acc = __builtin_fma(as[gg], bs[gg], acc);
         // fold now: deferred, every slot's shuffled operands would stay live to the end
         asm volatile("" : "+v"(acc));
     };
@@ -321,23 +355,32 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             lap(4);
             // p = beta p + r (two roundings); x += alpha_{it-1} p_{it-1} rides along
             launder();
+            // slots u < ulds: p at lds0 + 256 G u (their stores need no valid test either:
+            // a lane's LDS-prefix rows are its own chain rows or its chunk's)
+            auto pload = [&](int u) -> double {
+                return u < ulds ? lds_at(lds0() + 256u * G * u) : valid(u) ? ldc(code_of(rowof(u))) : 0.0;
+            };
+            auto pstore = [&](int u, double v) {
+                if (u < ulds) lds_put(lds0() + 256u * G * u, v);
+                else stc(code_of(rowof(u)), v);
+            };
             if (it == 0) {
 #pragma unroll
                 for (int u = 0; u < R; ++u)
-                    if (valid(u)) stc(code_of(rowof(u)), r[u]);
+                    if (valid(u)) pstore(u, r[u]);
             } else {
                 double pb4[R];  // p_old, kPre slots ahead (each slot reads and writes only its row)
 #pragma unroll
-                for (int u = 0; u < kPre && u < R; ++u) pb4[u] = valid(u) ? ldc(code_of(rowof(u))) : 0.0;
+                for (int u = 0; u < kPre && u < R; ++u) pb4[u] = pload(u);
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
-                    if (u + kPre < R) pb4[u + kPre] = valid(u + kPre) ? ldc(code_of(rowof(u + kPre))) : 0.0;
+                    if (u + kPre < R) pb4[u + kPre] = pload(u + kPre);
                     if (valid(u)) {
                         const double po = pb4[u];
                         const double t1 = alpha_prev * po;
                         x[u] = x[u] + t1;
                         const double pb = po * beta;
-                        stc(code_of(rowof(u)), pb + r[u]);
+                        pstore(u, pb + r[u]);
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -373,14 +416,14 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                         lb[u + kPre] = len_row(u + kPre);
                     }
                     double pv = 0.0, qv = 0.0;
-                    if (valid(u)) qv = spmv(rowof(u), eb[u], lb[u], pv);
+                    if (valid(u)) qv = spmv(rowof(u), eb[u], lb[u], pv, u);
                     chain_step(acc, pv, qv, u);
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 if (g == 0 && live) acc_pq[chain] = acc;
                 if (tail) {
                     double pt;
-                    side_q[tix] = spmv(trow, A.ell[trow], (int)A.rlen[trow], pt);
+                    side_q[tix] = spmv(trow, A.ell[trow], (int)A.rlen[trow], pt, -1);
                     side_p[tix] = pt;
                 }
             }
@@ -408,7 +451,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                     }
                     if (valid(u)) {
                         double pu;
-                        const double t2 = alpha * spmv(rowof(u), eb[u], lb[u], pu);
+                        const double t2 = alpha * spmv(rowof(u), eb[u], lb[u], pu, u);
                         r[u] = r[u] - t2;
                     }
                     chain_step(acc, r[u], r[u], u, true);
@@ -417,7 +460,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                 if (g == 0 && live) acc_rr[chain] = acc;
                 if (tail) {
                     double pt;
-                    const double t2 = alpha * spmv(trow, A.ell[trow], (int)A.rlen[trow], pt);
+                    const double t2 = alpha * spmv(trow, A.ell[trow], (int)A.rlen[trow], pt, -1);
                     side_r[tix] = side_r[tix] - t2;
                 }
             }
