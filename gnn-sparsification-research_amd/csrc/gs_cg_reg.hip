@@ -206,6 +206,10 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     A.ck = dch + 2 * kRegMaxChunks;
     A.cb = dch + 3 * kRegMaxChunks;
     A.prof = prof;
+    // 512-thread form: q kept in registers from the SpMV pass to the r update, x in Xc
+    // (GSPARSE_REG_QR=0: q recomputed in the r update, x in registers)
+    A.qreg = 1;
+    if (const char *e = getenv("GSPARSE_REG_QR")) A.qreg = atoi(e) != 0;
     if (NT == 512) {
         if (G == 1) regwide_launch_g1(A, rsel, ufast, dyn, (unsigned)slots, s);
         else if (G == 2) regwide_launch_g2(A, rsel, ufast, dyn, (unsigned)slots, s);

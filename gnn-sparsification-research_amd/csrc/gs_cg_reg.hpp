@@ -61,6 +61,7 @@ struct RegArgs {
     const int64_t *ca, *cl;  // chunk starts / lengths (device)
     const int64_t *ck, *cb;  // rows of each chunk whose p is in LDS (a prefix), and their LDS base
     long long *prof;      // optional: workgroup 0's phase times
+    int32_t qreg;         // 512-thread form: q in registers, x in Xc (see k_cg_regwide)
 };
 
 // A double held in two AGPRs.  r and x live there (read / written only through these

@@ -44,8 +44,12 @@ __device__ __forceinline__ double wide_readlane(double v, int ln) {
 
 // G threads per chain (power of two), R row slots per thread, UNIT: every
 // off-diagonal weight is -1.0 and every diagonal one fl((entries - 1) + 1e-6) (no
-// weights loaded; q_i folds -p_j and dg * p_i); else the ELL carries the weights
-template <int G, int R, bool UNIT>
+// weights loaded; q_i folds -p_j and dg * p_i); else the ELL carries the weights.
+// QR: q of the slots stays in the registers x used to hold, from the SpMV pass to the
+// r update (one SpMV per iteration instead of two); x lives in its output column of
+// Xc (L2 / Infinity Cache) and is updated there in the r-update pass, x += alpha p
+// in SciPy's own (non-deferred) order.
+template <int G, int R, bool UNIT, bool QR>
 __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     constexpr int CW = 64 / G;  // chains per wave
     extern __shared__ double lds[];
@@ -324,14 +328,25 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
 
     for (int64_t ci = blockIdx.x; ci < A.ncols; ci += gridDim.x) {
         const int64_t c = A.col0 + ci;
-        double r[R], x[R];
+        double r[R], x[QR ? 1 : R], qr[QR ? R : 1];
+        // QR: x of the slots in this column's Xc rows (raw buffer; rows past n dropped)
+        const __amdgpu_buffer_rsrc_t xrs =
+            __builtin_amdgcn_make_buffer_rsrc(A.Xc + ci * A.ldn, 0, (int)(A.n * 8), 0x00020000);
+        auto xload = [&](int u) -> double {
+            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xrs, base * 8, 256 * G * u, 0));
+        };
+        auto xstore = [&](int u, double v) {
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), xrs, base * 8, 256 * G * u, 0);
+        };
         // r = b.copy(); rho_0 = b.b
         {
             launder();
             double acc = 0.0;
 #pragma unroll
             for (int u = 0; u < R; ++u) {
-                x[u] = 0.0;
+                if constexpr (!QR) x[u] = 0.0;
+                else qr[u] = 0.0;
                 r[u] = valid(u) ? A.Rr[(int64_t)rowof(u) * A.ld + c] : 0.0;
                 chain_step(acc, r[u], r[u], u, true);
             }
@@ -377,8 +392,10 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                     if (u + kPre < R) pb4[u + kPre] = pload(u + kPre);
                     if (valid(u)) {
                         const double po = pb4[u];
-                        const double t1 = alpha_prev * po;
-                        x[u] = x[u] + t1;
+                        if constexpr (!QR) {
+                            const double t1 = alpha_prev * po;
+                            x[u] = x[u] + t1;
+                        }
                         const double pb = po * beta;
                         pstore(u, pb + r[u]);
                     }
@@ -390,8 +407,10 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                     stc(code_of(trow), side_r[tix]);
                 } else {
                     const double po = ldc(code_of(trow));
-                    const double t1 = alpha_prev * po;
-                    side_x[tix] = side_x[tix] + t1;
+                    if constexpr (!QR) {
+                        const double t1 = alpha_prev * po;
+                        side_x[tix] = side_x[tix] + t1;
+                    }
                     const double pb = po * beta;
                     stc(code_of(trow), pb + side_r[tix]);
                 }
@@ -417,6 +436,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                     }
                     double pv = 0.0, qv = 0.0;
                     if (valid(u)) qv = spmv(rowof(u), eb[u], lb[u], pv, u);
+                    if constexpr (QR) qr[u] = qv;
                     chain_step(acc, pv, qv, u);
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -432,6 +452,36 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             const double pq = finish(acc_pq, side_p, side_q);
             const double alpha = rho_cur / pq;
             lap(2);
+            // QR: x += alpha p (x from / to Xc, p from LDS), r -= alpha q (q in registers),
+            // chains of r.r
+            if constexpr (QR) {
+                launder();
+                double acc = 0.0;
+                double xb[R];  // x, kPre slots ahead (no read in the first iteration: x == 0)
+                if (it > 0) {
+#pragma unroll
+                    for (int u = 0; u < kPre && u < R; ++u) xb[u] = xload(u);
+                }
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    if (it > 0 && u + kPre < R) xb[u + kPre] = xload(u + kPre);
+                    if (valid(u)) {
+                        const double t1 = alpha * pload(u);
+                        xstore(u, (it > 0 ? xb[u] : 0.0) + t1);
+                        const double t2 = alpha * qr[u];
+                        r[u] = r[u] - t2;
+                    }
+                    chain_step(acc, r[u], r[u], u, true);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (g == 0 && live) acc_rr[chain] = acc;
+                if (tail) {
+                    const double t1 = alpha * side_p[tix];
+                    side_x[tix] = side_x[tix] + t1;
+                    const double t2 = alpha * side_q[tix];
+                    side_r[tix] = side_r[tix] - t2;
+                }
+            } else
             // r -= alpha q (q recomputed), chains of r.r
             {
                 launder();
@@ -474,6 +524,14 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         // x: b (||b|| == 0), 0 (no iteration), or the last pending update
         launder();
         double *xo = A.Xc + ci * A.ldn;
+        if constexpr (QR) {  // x is in place after any iteration
+            if (bn == 0.0 || done == 0) {
+#pragma unroll
+                for (int u = 0; u < R; ++u)
+                    if (valid(u)) xstore(u, bn == 0.0 ? r[u] : 0.0);
+            }
+            if (tail) xo[trow] = bn == 0.0 ? side_r[tix] : done == 0 ? 0.0 : side_x[tix];
+        } else {
 #pragma unroll
         for (int u = 0; u < R; ++u)
             if (valid(u)) {
@@ -497,6 +555,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             }
             xo[trow] = v;
         }
+        }
         if (tid == 0) A.iters[c] = done;
         __syncthreads();  // the next column's b.b chains reuse acc_rr / side_r
     }
@@ -513,17 +572,22 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn)); \
             kern<<<slots, kRegThreads, dyn, s>>>(A);                                          \
         };                                                                                    \
-        if (unit) {                                                                           \
-            if (R == 16) go(k_cg_regwide<G_, 16, true>);                                      \
-            else if (R == 24) go(k_cg_regwide<G_, 24, true>);                                 \
-            else if (R == 32) go(k_cg_regwide<G_, 32, true>);                                 \
-            else go(k_cg_regwide<G_, 44, true>);                                              \
-        } else {                                                                              \
-            if (R == 16) go(k_cg_regwide<G_, 16, false>);                                     \
-            else if (R == 24) go(k_cg_regwide<G_, 24, false>);                                \
-            else if (R == 32) go(k_cg_regwide<G_, 32, false>);                                \
-            else go(k_cg_regwide<G_, 44, false>);                                             \
-        }                                                                                     \
+        auto pick = [&](auto qr) {                                                            \
+            constexpr bool Q = decltype(qr)::value;                                           \
+            if (unit) {                                                                       \
+                if (R == 16) go(k_cg_regwide<G_, 16, true, Q>);                               \
+                else if (R == 24) go(k_cg_regwide<G_, 24, true, Q>);                          \
+                else if (R == 32) go(k_cg_regwide<G_, 32, true, Q>);                          \
+                else go(k_cg_regwide<G_, 44, true, Q>);                                       \
+            } else {                                                                          \
+                if (R == 16) go(k_cg_regwide<G_, 16, false, Q>);                              \
+                else if (R == 24) go(k_cg_regwide<G_, 24, false, Q>);                         \
+                else if (R == 32) go(k_cg_regwide<G_, 32, false, Q>);                         \
+                else go(k_cg_regwide<G_, 44, false, Q>);                                      \
+            }                                                                                 \
+        };                                                                                    \
+        if (A.qreg) pick(std::true_type{});                                                   \
+        else pick(std::false_type{});                                                         \
     }
 
 }  // namespace gs

@@ -59,16 +59,19 @@ def test_approx_er_bit_exact(gs, name):
     assert bits_equal(er, ref), float(np.max(np.abs(er - ref) / np.abs(ref)))
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4", "5", "5n"])
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4", "5", "5n", "5r"])
 @pytest.mark.parametrize("name", ["karate_csr", "rmat10", "directed_dup", "roman2000"])
 def test_approx_er_all_cg_modes(gs, name, mode, monkeypatch):
     """q recomputed in the update kernel (0), stored by the fused p/q kernel (1),
     split p stream + SpMV (2, 3), the resident per-column solver (4), or the
     register-resident one (5: one BLAS chunk here, 8 threads per chain; 5n: its
-    256-thread form) -- the same bits in every mode."""
+    256-thread form; 5r: q recomputed instead of kept in registers) -- the same bits in every mode."""
     if mode == "5n":
         mode = "5"
         monkeypatch.setenv("GSPARSE_REG_NT", "256")
+    if mode == "5r":  # 512-thread form with q recomputed in the r update, x in registers
+        mode = "5"
+        monkeypatch.setenv("GSPARSE_REG_QR", "0")
     monkeypatch.setenv("GSPARSE_CG_MODE", mode)
     g = load_golden(name)
     sp_, _ = make(gs, g, with_x=False)
@@ -126,13 +129,17 @@ def chunked_er():
                                  {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_NT": "256",
                                   "GSPARSE_RES_UNIT": "0"},
                                  {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_NT": "256",
-                                  "GSPARSE_REG_KEEP": "40"}],
+                                  "GSPARSE_REG_KEEP": "40"},
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_QR": "0"},
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_QR": "0", "GSPARSE_RES_UNIT": "0"},
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_QR": "0", "GSPARSE_REG_KEEP": "40"}],
                          ids=["m0", "m1", "m3", "m4", "m4-ell", "m4-q-global", "m4-7slots",
                               "m4-weighted-sell", "m4-weighted-ell", "m4-slices-global",
                               "m4-rb4w4", "m4-rb4w4-weighted", "m4-diag-loaded", "m4-w6", "m4-w8",
                               "m5", "m5-weighted", "m5-diag-loaded", "m5-7slots", "m5-p-global",
                               "m5-p-all-global-weighted", "m5-narrow", "m5-narrow-weighted",
-                              "m5-narrow-p-global"])
+                              "m5-narrow-p-global", "m5-q-recomputed", "m5-q-recomputed-weighted",
+                              "m5-q-recomputed-p-global"])
 @pytest.mark.parametrize("threads", [3, 8])
 @pytest.mark.parametrize("graph", ["unit", "dup", "hub"])
 def test_approx_er_blas_chunks_vs_oracle(gs, chunked_er, graph, threads, env, monkeypatch):
