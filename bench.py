@@ -40,6 +40,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# aggregate LDS read rate: ds_read_b64 moves 256 B/clk/CU (MI355X_MICROARCH.md, LDS table)
+# x 256 CUs x 2.4 GHz -- the on-chip bound of the register-resident CG solver
+LDS_PEAK_GBS = 256 * 256 * 2.4
 # MI355X dense fp64 matrix peak as AMD publishes it (the microarchitecture guide lists
 # no fp64 figure); a register-only v_mfma_f64_16x16x4_f64 loop sustains 49-50 on the
 # box (tools/mfma_f64_peak.hip, profiles/r01j_mfma_f64_peak.log).
@@ -885,6 +888,13 @@ def main():
                     "avg_launch_ms": round(avg_ms, 5),
                     "algorithmic_bytes_per_launch": bytes_per, "launches": p["launches"]}
         add_traffic(roofline, traffic, tsrc, avg_ms)
+        if name == "cg_reg":
+            # B_ER's bytes move through LDS and registers in this solver (p gathered from
+            # LDS, r / x / q in registers); against the LDS rate it is latency-bound, not
+            # bandwidth-bound (SQ counters)
+            roofline["on_chip"] = {"bound": "lds", "achieved": round(achieved, 1),
+                                   "peak": round(LDS_PEAK_GBS, 1), "unit": "GB/s",
+                                   "frac": round(achieved / LDS_PEAK_GBS, 4)}
     kernels = {k2: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k2, v in prof.items()}
 
     result = {
