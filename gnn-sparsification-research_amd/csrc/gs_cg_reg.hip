@@ -17,8 +17,10 @@ __global__ void k_ell8_count(int32_t n, const int64_t *__restrict__ lp, int64_t 
 }
 
 // p code of column c: its LDS slot when c is in its chunk's LDS-resident prefix,
-// else 0x8000 | c (chunk table: starts, lengths, prefixes, LDS bases)
+// else 0x8000 | c (chunk table: starts, lengths, prefixes, LDS bases).  A split part's
+// table holds only its own chunks: columns outside them are global (other parts' rows)
 __device__ __forceinline__ uint32_t p_code(int32_t c, int T, const int64_t *__restrict__ tab) {
+    if (c < tab[0] || c >= tab[T - 1] + tab[kRegMaxChunks + T - 1]) return 0x8000u | (uint32_t)c;
     int t = 0;
     while (t + 1 < T && c >= tab[t + 1]) ++t;
     const int64_t o = c - tab[t];
@@ -45,13 +47,13 @@ __device__ __forceinline__ int row_dslot(int32_t c, int T, const int64_t *__rest
 
 // dslot0 >= 0 (unit form): the diagonal entry's code is the owner thread's diagonal
 // slot dslot0 + tid instead of the row's p code
-__global__ void k_ell8_fill(int32_t n, int T, const int64_t *__restrict__ tab, uint32_t pad,
+__global__ void k_ell8_fill(int32_t r0, int32_t n, int T, const int64_t *__restrict__ tab, uint32_t pad,
                             int G, int dmul, int32_t dslot0, const int64_t *__restrict__ lp,
                             const int32_t *__restrict__ li, const double *__restrict__ lv,
                             const int64_t *__restrict__ optr, uint4 *__restrict__ ell,
                             double *__restrict__ ellv, uint16_t *__restrict__ ocol,
                             double *__restrict__ oval) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+    for (int64_t i = r0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e0 = lp[i], len = lp[i + 1] - e0;
         const uint32_t dcode = dslot0 >= 0 ? (uint32_t)(dslot0 + row_dslot((int32_t)i, T, tab, G, dmul)) : 0u;
@@ -175,16 +177,75 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     double *ellv = ufast ? nullptr : (double *)c->buf("er_reg_ellv").ensure(sizeof(double) * 8 * n);
     auto *ocol = (uint16_t *)c->buf("er_reg_ocol").ensure(sizeof(uint16_t) * (nov + 1));
     double *oval = ufast ? nullptr : (double *)c->buf("er_reg_oval").ensure(sizeof(double) * (nov + 1));
-    k_ell8_fill<<<grid_for(n, 256, 8192), 256, 0, s>>>((int32_t)n, T, dch, pad, G, NT == 256 ? 2 : 1,
+    k_ell8_fill<<<grid_for(n, 256, 8192), 256, 0, s>>>(0, (int32_t)n, T, dch, pad, G, NT == 256 ? 2 : 1,
                                                       ufast ? (int32_t)zs + 2 : -1, lp, li, lv, optr,
                                                       ell, ellv, ocol, oval);
     GS_HIP(hipGetLastError());
-    double *pg = (double *)c->buf("er_reg_pg").ensure(sizeof(double) * (size_t)slots * ldn);
     RegArgs A{};
+    // 512-thread form: q kept in registers from the SpMV pass to the r update, x in Xc
+    // (GSPARSE_REG_QR=0: q recomputed in the r update, x in registers)
+    A.qreg = 1;
+    if (const char *e = getenv("GSPARSE_REG_QR")) A.qreg = atoi(e) != 0;
+    // Split plan: the last round of columns, when it leaves at least half the CUs idle,
+    // runs as groups of P workgroups per column (k_cg_regwide<..., SPLIT>), each part a
+    // contiguous range of the BLAS chunks with all its rows' p in LDS.
+    // GSPARSE_REG_SPLIT=0: never; =P (>= 2): every column in P parts (tests).
+    int ncu = 256;
+    GS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+    int P = 0;
+    int64_t W = ncols;  // columns solved whole (the first W), the rest split
+    if (NT == 512 && A.qreg && T >= 2 && ncols > 0) {
+        const char *se = getenv("GSPARSE_REG_SPLIT");
+        const int forced = se ? atoi(se) : -1;
+        if (forced >= 2) {
+            P = std::min(forced, T);
+            W = 0;
+        } else if (forced < 0 && !getenv("GSPARSE_CG_SLOTS")) {
+            const int64_t rounds = (ncols + ncu - 1) / ncu;
+            const int64_t tailc = ncols - (rounds - 1) * ncu;
+            const int p = (int)std::min<int64_t>(T, ncu / tailc);
+            if (p >= 2) {
+                P = p;
+                W = (rounds - 1) * ncu;
+            }
+        }
+    }
+    // parts: chunk ranges as equal as possible; one geometry (G, R) for all of them
+    int pc0[kRegMaxChunks + 1] = {}, Gs = 0, Rs = 0;
+    size_t dyns = 0;
+    if (P >= 2) {
+        int tmax = 0;
+        for (int h = 0, at = 0; h < P; ++h) {
+            pc0[h] = at;
+            at += T / P + (h < T % P ? 1 : 0);
+            tmax = std::max(tmax, at - pc0[h]);
+        }
+        pc0[P] = T;
+        int64_t plen[kRegMaxChunks];
+        for (int t = 0; t < tmax; ++t) plen[t] = 0;
+        for (int h = 0; h < P; ++h)
+            for (int t = pc0[h]; t < pc0[h + 1]; ++t)
+                plen[t - pc0[h]] = std::max<int64_t>(plen[t - pc0[h]], hlen[t]);
+        const int rr = reg_geometry(512, tmax, plen, Gs);
+        Rs = rr < 0 ? -1 : rr <= 16 ? 16 : rr <= 24 ? 24 : rr <= 32 ? 32 : rr <= 44 ? 44 : -1;
+        for (int h = 0; h < P; ++h) {
+            int64_t rows = 0;
+            for (int t = pc0[h]; t < pc0[h + 1]; ++t) rows += hlen[t];
+            const int th = pc0[h + 1] - pc0[h];
+            dyns = std::max(dyns, sizeof(double) * ((size_t)rows + 2 + dsl + 6 * 32 * (size_t)th +
+                                                    2 * kRegMaxChunks + 1));
+        }
+        if (Rs < 0 || Gs < 4 || dyns > lds_max) {  // does not fit: solve every column whole
+            P = 0;
+            W = ncols;
+        }
+    }
+    const int64_t wslots = P ? std::min<int64_t>(ncu, std::max<int64_t>(W, 1)) : slots;
+    double *pg = (double *)c->buf("er_reg_pg").ensure(sizeof(double) * (size_t)std::max<int64_t>(wslots, 1) * ldn);
     A.ld = ld;
     A.ldn = ldn;
     A.col0 = col0;
-    A.ncols = ncols;
+    A.ncols = W;
     A.n = (int32_t)n;
     A.Rr = Rr;
     A.Xc = Xc;
@@ -206,20 +267,89 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     A.ck = dch + 2 * kRegMaxChunks;
     A.cb = dch + 3 * kRegMaxChunks;
     A.prof = prof;
-    // 512-thread form: q kept in registers from the SpMV pass to the r update, x in Xc
-    // (GSPARSE_REG_QR=0: q recomputed in the r update, x in registers)
-    A.qreg = 1;
-    if (const char *e = getenv("GSPARSE_REG_QR")) A.qreg = atoi(e) != 0;
-    if (NT == 512) {
-        if (G == 1) regwide_launch_g1(A, rsel, ufast, dyn, (unsigned)slots, s);
-        else if (G == 2) regwide_launch_g2(A, rsel, ufast, dyn, (unsigned)slots, s);
-        else if (G == 4) regwide_launch_g4(A, rsel, ufast, dyn, (unsigned)slots, s);
-        else regwide_launch_g8(A, rsel, ufast, dyn, (unsigned)slots, s);
-    } else if (G == 1) regres_launch_g1(A, rsel, ufast, dyn, (unsigned)slots, s);
-    else if (G == 2) regres_launch_g2(A, rsel, ufast, dyn, (unsigned)slots, s);
-    else if (G == 4) regres_launch_g4(A, rsel, ufast, dyn, (unsigned)slots, s);
-    else regres_launch_g8(A, rsel, ufast, dyn, (unsigned)slots, s);
+    if (W > 0) {
+        if (NT == 512) {
+            if (G == 1) regwide_launch_g1(A, rsel, ufast, dyn, (unsigned)wslots, s);
+            else if (G == 2) regwide_launch_g2(A, rsel, ufast, dyn, (unsigned)wslots, s);
+            else if (G == 4) regwide_launch_g4(A, rsel, ufast, dyn, (unsigned)wslots, s);
+            else regwide_launch_g8(A, rsel, ufast, dyn, (unsigned)wslots, s);
+        } else if (G == 1) regres_launch_g1(A, rsel, ufast, dyn, (unsigned)wslots, s);
+        else if (G == 2) regres_launch_g2(A, rsel, ufast, dyn, (unsigned)wslots, s);
+        else if (G == 4) regres_launch_g4(A, rsel, ufast, dyn, (unsigned)wslots, s);
+        else regres_launch_g8(A, rsel, ufast, dyn, (unsigned)wslots, s);
+        GS_HIP(hipGetLastError());
+    }
+    if (P < 2) return;
+
+    // split tail: per-part chunk tables (LDS layout: the part's rows from slot 0, then
+    // the zero slot) and an ELL whose codes each row's part resolves
+    const int64_t tailn = ncols - W;
+    const int64_t groups = std::min<int64_t>(tailn, ncu / P);
+    int32_t hpt[kRegMaxChunks * kRegPartTab] = {};
+    int64_t htab[kRegMaxChunks][4 * kRegMaxChunks] = {};
+    for (int h = 0; h < P; ++h) {
+        int32_t *pt = hpt + h * kRegPartTab;
+        int64_t zsh = 0;
+        for (int t = pc0[h]; t < pc0[h + 1]; ++t) {
+            const int tl = t - pc0[h];
+            pt[tl] = (int32_t)ha[t];
+            pt[kRegMaxChunks + tl] = (int32_t)hlen[t];
+            pt[2 * kRegMaxChunks + tl] = (int32_t)hlen[t];
+            pt[3 * kRegMaxChunks + tl] = (int32_t)zsh;
+            htab[h][tl] = ha[t];
+            htab[h][kRegMaxChunks + tl] = hlen[t];
+            htab[h][2 * kRegMaxChunks + tl] = hlen[t];
+            htab[h][3 * kRegMaxChunks + tl] = zsh;
+            zsh += hlen[t];
+        }
+        pt[4 * kRegMaxChunks] = pc0[h + 1] - pc0[h];
+        pt[4 * kRegMaxChunks + 1] = (int32_t)zsh;
+        pt[4 * kRegMaxChunks + 2] = pc0[h];
+    }
+    auto *dpt = (int32_t *)c->buf("er_reg_split_ptab").ensure(sizeof(hpt));
+    auto *dtab = (int64_t *)c->buf("er_reg_split_tab").ensure(sizeof(htab));
+    GS_HIP(hipMemcpy(dpt, hpt, sizeof(hpt), hipMemcpyHostToDevice));
+    GS_HIP(hipMemcpy(dtab, htab, sizeof(htab), hipMemcpyHostToDevice));
+    auto *ells = (uint4 *)c->buf("er_reg_split_ell").ensure(sizeof(uint4) * n);
+    double *ellvs = ufast ? nullptr : (double *)c->buf("er_reg_split_ellv").ensure(sizeof(double) * 8 * n);
+    auto *ocols = (uint16_t *)c->buf("er_reg_split_ocol").ensure(sizeof(uint16_t) * (nov + 1));
+    double *ovals = ufast ? nullptr : (double *)c->buf("er_reg_split_oval").ensure(sizeof(double) * (nov + 1));
+    for (int h = 0; h < P; ++h) {
+        const int32_t r0 = (int32_t)ha[pc0[h]];
+        const int32_t r1 = (int32_t)(ha[pc0[h + 1] - 1] + hlen[pc0[h + 1] - 1]);
+        const int32_t zsh = hpt[h * kRegPartTab + 4 * kRegMaxChunks + 1];
+        k_ell8_fill<<<grid_for(r1 - r0, 256, 8192), 256, 0, s>>>(
+            r0, r1, pc0[h + 1] - pc0[h], dtab + h * 4 * kRegMaxChunks, (uint32_t)zsh, Gs, 1,
+            ufast ? zsh + 2 : -1, lp, li, lv, optr, ells, ellvs, ocols, ovals);
+        GS_HIP(hipGetLastError());
+    }
+    double *pgs = (double *)c->buf("er_reg_split_pg").ensure(sizeof(double) * (size_t)groups * 2 * ldn);
+    double *xch = (double *)c->buf("er_reg_split_xch").ensure(sizeof(double) * (size_t)groups * 2 * kRegMaxChunks);
+    auto *flg = (int32_t *)c->buf("er_reg_split_flags").ensure(sizeof(int32_t) * ((size_t)groups * P + 1));
+    GS_HIP(hipMemsetAsync(flg, 0, sizeof(int32_t) * ((size_t)groups * P + 1), s));
+    RegArgs B = A;
+    B.col0 = col0 + W;
+    B.ncols = tailn;
+    B.Xc = Xc + W * ldn;
+    B.pg = pgs;
+    B.ell = ells;
+    B.ellv = ellvs;
+    B.ocol = ocols;
+    B.oval = ovals;
+    B.prof = nullptr;
+    B.P = P;
+    B.ptab = dpt;
+    B.xch = xch;
+    B.flags = flg;
+    B.abortf = flg + (size_t)groups * P;
+    const unsigned grid = (unsigned)(groups * P);
+    if (Gs == 4) regwide_split_launch_g4(B, Rs, ufast, dyns, grid, s);
+    else regwide_split_launch_g8(B, Rs, ufast, dyns, grid, s);
     GS_HIP(hipGetLastError());
+    int32_t aborted = 0;
+    GS_HIP(hipMemcpyAsync(&aborted, B.abortf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    GS_CHECK(!aborted, GS_EHIP, "split CG: a hand-off between the %d parts of a column timed out", P);
 }
 
 }  // namespace gs

@@ -62,7 +62,14 @@ struct RegArgs {
     const int64_t *ck, *cb;  // rows of each chunk whose p is in LDS (a prefix), and their LDS base
     long long *prof;      // optional: workgroup 0's phase times
     int32_t qreg;         // 512-thread form: q in registers, x in Xc (see k_cg_regwide)
+    // split form (k_cg_regwide<..., SPLIT>): P parts per column
+    int32_t P;
+    const int32_t *ptab;  // [P][kRegPartTab]: the part's chunk table, chunks, zero slot, first chunk
+    double *xch;          // [groups][2][kRegMaxChunks] chunk dots by hand-off parity
+    int32_t *flags;       // [groups][P] hand-off sequence numbers (zeroed before the launch)
+    int32_t *abortf;      // set when a hand-off poll gave up
 };
+static constexpr int kRegPartTab = 4 * kRegMaxChunks + 4;
 
 // A double held in two AGPRs.  r and x live there (read / written only through these
 // asm moves, so the allocator keeps their home in the accumulation registers): with
@@ -574,6 +581,9 @@ GS_REGWIDE_LAUNCH_DECL(2)
 GS_REGWIDE_LAUNCH_DECL(4)
 GS_REGWIDE_LAUNCH_DECL(8)
 #undef GS_REGWIDE_LAUNCH_DECL
+// split form, 4 or 8 threads per chain (gs_cg_reg_g4.hip, gs_cg_reg_g8.hip)
+void regwide_split_launch_g4(const RegArgs &A, int R, bool unit, size_t dyn, unsigned grid, hipStream_t s);
+void regwide_split_launch_g8(const RegArgs &A, int R, bool unit, size_t dyn, unsigned grid, hipStream_t s);
 
 // one launch of the kernel: R row slots (24 / 48 / 64 / 88), unit or weighted form
 #define GS_REGRES_LAUNCH_DEF(G_)                                                              \

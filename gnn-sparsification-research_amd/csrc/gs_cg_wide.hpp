@@ -49,26 +49,47 @@ __device__ __forceinline__ double wide_readlane(double v, int ln) {
 // r update (one SpMV per iteration instead of two); x lives in its output column of
 // Xc (L2 / Infinity Cache) and is updated there in the r-update pass, x += alpha p
 // in SciPy's own (non-deferred) order.
-template <int G, int R, bool UNIT, bool QR>
+// SPLIT: a column is solved by a group of A.P workgroups (parts), part h owning a
+// contiguous range of the BLAS chunks (all its rows' p in LDS).  Every part publishes
+// its rows' p (write-through sc1 stores, buffer by iteration parity) for the other
+// parts' SpMV, and its chunk dots (buffer by hand-off parity); three flag hand-offs per
+// iteration (after the p update, before each dot's chunk sum) -- MI355X_MICROARCH.md's
+// drained-sc1 recipe: sc1 payload, s_waitcnt vmcnt(0), barrier, one sc1 flag store, sc1
+// polls.  The chunk dots are added in global chunk order, so the bits are those of
+// the one-workgroup solve.  Used for the last, partly occupied round of columns.
+template <int G, int R, bool UNIT, bool QR, bool SPLIT = false>
 __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     constexpr int CW = 64 / G;  // chains per wave
     extern __shared__ double lds[];
-    const int T = A.T, nch = 32 * T;
+    const int part = SPLIT ? (int)(blockIdx.x % (unsigned)A.P) : 0;
+    const int group = SPLIT ? (int)(blockIdx.x / (unsigned)A.P) : (int)blockIdx.x;
+    const int ngroups = SPLIT ? (int)(gridDim.x / (unsigned)A.P) : (int)gridDim.x;
+    // SPLIT: this part's chunk table, [4][kRegMaxChunks] then chunks, zero slot, first chunk
+    const int32_t *ptab = SPLIT ? A.ptab + part * kRegPartTab : nullptr;
+    const int T = SPLIT ? ptab[4 * kRegMaxChunks] : A.T, nch = 32 * T;
+    const int zslot = SPLIT ? ptab[4 * kRegMaxChunks + 1] : A.zslot;  // LDS slot holding 0.0
+    const int t0g = SPLIT ? ptab[4 * kRegMaxChunks + 2] : 0;          // global index of chunk 0
+    const int Tg = SPLIT ? A.T : T;                                    // chunks of the whole column
     // LDS: p at offset 0 (a gather's address is its code * 8), the zero and scratch
     // slots, (unit form) one diagonal slot per thread, then chain sums, tail rows and
     // the chunk table
     double *sp = lds;
-    double *acc_pq = lds + A.zslot + 2 + (UNIT ? kRegThreads : 0), *acc_rr = acc_pq + nch;
+    double *acc_pq = lds + zslot + 2 + (UNIT ? kRegThreads : 0), *acc_rr = acc_pq + nch;
     double *side_p = acc_pq + 2 * nch, *side_q = acc_pq + 3 * nch, *side_r = acc_pq + 4 * nch;
     double *side_x = acc_pq + 5 * nch;  // tail rows' r lives in side_r, x here
-    // [4][kRegMaxChunks]: starts, lengths, LDS-resident prefix, its LDS base
+    // [4][kRegMaxChunks]: starts, lengths, LDS-resident prefix, its LDS base (SPLIT: then
+    // the hand-off verdict word)
     int *s_ch = reinterpret_cast<int *>(acc_pq + 6 * nch);
     const int tid = threadIdx.x, lane = tid & 63;
     if (tid < T) {
-        s_ch[tid] = (int)A.ca[tid];
-        s_ch[kRegMaxChunks + tid] = (int)A.cl[tid];
-        s_ch[2 * kRegMaxChunks + tid] = (int)A.ck[tid];
-        s_ch[3 * kRegMaxChunks + tid] = (int)A.cb[tid];
+        if constexpr (SPLIT) {
+            for (int k4 = 0; k4 < 4; ++k4) s_ch[k4 * kRegMaxChunks + tid] = ptab[k4 * kRegMaxChunks + tid];
+        } else {
+            s_ch[tid] = (int)A.ca[tid];
+            s_ch[kRegMaxChunks + tid] = (int)A.cl[tid];
+            s_ch[2 * kRegMaxChunks + tid] = (int)A.ck[tid];
+            s_ch[3 * kRegMaxChunks + tid] = (int)A.cb[tid];
+        }
     }
     __syncthreads();
     const int jj = lane % CW, g = lane / CW;
@@ -107,18 +128,21 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         ulds = __builtin_amdgcn_readfirstlane(uk);
     }
     auto lds0 = [&]() -> uint32_t { return (uint32_t)(lbase_t + base - ca_t) * 8u; };
-    const int zslot = A.zslot;  // LDS slot holding 0.0 (the ELL padding code)
     // explicit address spaces: a select between an LDS and a global pointer would
     // become one (slow) flat load
     typedef __attribute__((address_space(3))) double lds_f64;
     auto lds_at = [](uint32_t a) -> double { return *(lds_f64 *)(uintptr_t)a; };
     auto lds_put = [](uint32_t a, double v) { *(lds_f64 *)(uintptr_t)a = v; };
     lds_f64 *spl = (lds_f64 *)sp;
-    double *pgw = A.pg + (int64_t)blockIdx.x * A.ldn;
-    // rows of p outside LDS: raw buffer, offsets past its size read 0 / drop the store
+    // rows of p outside LDS: raw buffer, offsets past its size read 0 / drop the store.
+    // SPLIT: the group's published p (two iteration-parity halves, poff selects one;
+    // sc1 loads and stores, so no CU's L1 serves a stale line)
+    double *pgw = A.pg + (int64_t)group * (SPLIT ? 2 : 1) * A.ldn;
     const __amdgpu_buffer_rsrc_t prs =
-        __builtin_amdgcn_make_buffer_rsrc(pgw, 0, (int)(A.ldn * 8), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(pgw, 0, (int)(A.ldn * 8 * (SPLIT ? 2 : 1)), 0x00020000);
     constexpr int kOob = (int)0x80000000;
+    constexpr int kAux = SPLIT ? 16 : 0;  // cache policy of the global p accesses (16: sc1)
+    int poff = 0;                          // SPLIT: byte offset of this iteration's p half
     // s_waitcnt vmcnt(0) inside a branch that loads p from the global slot: the waitcnt
     // pass then sees no pending load at the join, and the ELL rows prefetched for the
     // next slots stay in flight (otherwise every slot waits for them: vmcnt(0))
@@ -143,7 +167,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         double v = spl[cd < 0x8000 ? cd : zslot];
         if (__builtin_amdgcn_ballot_w64(cd >= 0x8000)) {
             const double vg = __builtin_bit_cast(
-                double, __builtin_amdgcn_raw_buffer_load_b64(prs, cd < 0x8000 ? kOob : (cd & 0x7fff) * 8, 0, 0));
+                double, __builtin_amdgcn_raw_buffer_load_b64(prs, cd < 0x8000 ? kOob : (cd & 0x7fff) * 8 + poff, 0, kAux));
             v = cd < 0x8000 ? v : vg;
             vm_drain();
         }
@@ -154,7 +178,13 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         if (__builtin_amdgcn_ballot_w64(cd >= 0x8000))
             __builtin_amdgcn_raw_buffer_store_b64(
                 __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), prs,
-                cd < 0x8000 ? kOob : (cd & 0x7fff) * 8, 0, 0);
+                cd < 0x8000 ? kOob : (cd & 0x7fff) * 8 + poff, 0, kAux);
+    };
+    // SPLIT: publish p of an own row (kept in LDS) for the other parts
+    auto publish = [&](int row, double v) {
+        if constexpr (SPLIT)
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), prs, row * 8 + poff, 0, 16);
     };
     auto valid = [&](int u) { return u < uc; };
     auto ell_row = [&](int u) -> uint4 {
@@ -203,7 +233,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             for (int k = 0; k < 8; ++k) {
                 const bool gk = ad[k] >= 0x8000u * 8;
                 const double vg = __builtin_bit_cast(
-                    double, __builtin_amdgcn_raw_buffer_load_b64(prs, gk ? (int)(ad[k] & 0x3fff8u) : kOob, 0, 0));
+                    double, __builtin_amdgcn_raw_buffer_load_b64(prs, gk ? (int)(ad[k] & 0x3fff8u) + poff : kOob, 0, kAux));
                 pv[k] = gk ? vg : pv[k];
             }
             if (!UNIT && !fast) pown = ldc(self);
@@ -263,6 +293,44 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         asm volatile("" : "+v"(acc));
     };
 
+    // SPLIT hand-off: every wave drains its (sc1) stores, then one lane raises this
+    // part's flag to the next sequence number and polls the group's other flags.  A
+    // poll that never matches (a part that cannot arrive) gives up after a few seconds
+    // and sets the abort word: from then on this workgroup's hand-offs are barriers
+    // only, so the launch runs out (its results are discarded, the host reports the
+    // abort) instead of hanging the GPU.  (No early return: a divergent exit from the
+    // column loop breaks the uniform-register allocation of this kernel.)
+    int32_t hseq = 0;
+    bool bad = false;
+    int32_t *gflags = SPLIT ? A.flags + (int64_t)group * A.P : nullptr;
+    auto handoff = [&]() {
+        ++hseq;
+        vm_drain();
+        __syncthreads();
+        if (tid == 0 && !bad) {
+            int verdict = 0;
+            __hip_atomic_store(gflags + part, hseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int q = 0; q < A.P && !verdict; ++q) {
+                if (q == part) continue;
+                for (int spin = 0; __hip_atomic_load(gflags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hseq;
+                     ++spin) {
+                    if (spin > (1 << 22)) {
+                        verdict = 1;
+                        __hip_atomic_store(A.abortf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            s_ch[4 * kRegMaxChunks] = verdict;
+        }
+        __syncthreads();
+        bad = bad || s_ch[4 * kRegMaxChunks] != 0;
+    };
+    // SPLIT: chunk dots of the group, [hand-off parity][global chunk]
+    const __amdgpu_buffer_rsrc_t xcs = __builtin_amdgcn_make_buffer_rsrc(
+        SPLIT ? A.xch + (int64_t)group * 2 * kRegMaxChunks : A.pg, 0, 2 * kRegMaxChunks * 8, 0x00020000);
+
     // OpenBLAS finish of one dot (every wave computes it; lane = chunk)
     // lanes 4 t + l (t < T, l < 4) fold c4[l] of chunk t with all their LDS loads in
     // flight; lane 4 t collects its quad's four (DPP) and adds the chunk's FMA tail; the
@@ -312,6 +380,21 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                     if (i0 + i < nt) dot = __builtin_fma(tb[i], ta[i], dot);
             }
         }
+        if constexpr (SPLIT) {
+            // publish this part's chunk dots (wave 0, lane 4 t), hand off, then every wave
+            // adds all Tg chunk dots of the column in global chunk order
+            const int slot = ((hseq + 1) & 1) * kRegMaxChunks;
+            if (tid < 64 && lv && l == 0)
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, dot), xcs,
+                    (slot + t0g + tq) * 8, 0, 16);
+            handoff();
+            const double all = __builtin_bit_cast(
+                double, __builtin_amdgcn_raw_buffer_load_b64(xcs, lane < Tg ? (slot + lane) * 8 : kOob, 0, 16));
+            double total = 0.0;
+            for (int tt = 0; tt < Tg; ++tt) total = total + wide_readlane(all, tt);
+            return total;
+        }
         if (T == 1) return wide_readlane(dot, 0);
         double total = 0.0;
         for (int tt = 0; tt < T; ++tt) total = total + wide_readlane(dot, 4 * tt);
@@ -326,7 +409,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         tmark = tn;
     };
 
-    for (int64_t ci = blockIdx.x; ci < A.ncols; ci += gridDim.x) {
+    for (int64_t ci = group; ci < A.ncols; ci += ngroups) {
         const int64_t c = A.col0 + ci;
         double r[R], x[QR ? 1 : R], qr[QR ? R : 1];
         // QR: x of the slots in this column's Xc rows (raw buffer; rows past n dropped)
@@ -367,6 +450,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             if (it > 0 && __builtin_sqrt(rr) < atol) break;  // loop-top test
             const double rho_cur = rr;
             const double beta = it > 0 ? rho_cur / rho_prev : 0.0;
+            if constexpr (SPLIT) poff = (it & 1) * (int)A.ldn * 8;
             lap(4);
             // p = beta p + r (two roundings); x += alpha_{it-1} p_{it-1} rides along
             launder();
@@ -378,6 +462,9 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             auto pstore = [&](int u, double v) {
                 if (u < ulds) lds_put(lds0() + 256u * G * u, v);
                 else stc(code_of(rowof(u)), v);
+                if constexpr (SPLIT) {
+                    if (valid(u)) publish(rowof(u), v);
+                }
             };
             if (it == 0) {
 #pragma unroll
@@ -405,6 +492,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             if (tail) {
                 if (it == 0) {
                     stc(code_of(trow), side_r[tix]);
+                    publish(trow, side_r[tix]);
                 } else {
                     const double po = ldc(code_of(trow));
                     if constexpr (!QR) {
@@ -413,9 +501,14 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                     }
                     const double pb = po * beta;
                     stc(code_of(trow), pb + side_r[tix]);
+                    publish(trow, pb + side_r[tix]);
                 }
             }
-            __syncthreads();
+            if constexpr (SPLIT) {
+                handoff();  // every part's p published before any SpMV reads it
+            } else {
+                __syncthreads();
+            }
             lap(0);
             // q = L_reg p and the chains of p.q
             {
@@ -556,7 +649,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             xo[trow] = v;
         }
         }
-        if (tid == 0) A.iters[c] = done;
+        if (tid == 0 && part == 0) A.iters[c] = done;
         __syncthreads();  // the next column's b.b chains reuse acc_rr / side_r
     }
     if (A.prof && blockIdx.x == 0 && tid == 0)
@@ -588,6 +681,28 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         };                                                                                    \
         if (A.qreg) pick(std::true_type{});                                                   \
         else pick(std::false_type{});                                                         \
+    }
+
+// one launch of the split form (q in registers), grid = groups x A.P workgroups
+#define GS_REGWIDE_SPLIT_DEF(G_)                                                               \
+    void regwide_split_launch_g##G_(const RegArgs &A, int R, bool unit, size_t dyn,            \
+                                    unsigned grid, hipStream_t s) {                            \
+        auto go = [&](auto kern) {                                                             \
+            GS_HIP(hipFuncSetAttribute((const void *)kern,                                     \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));  \
+            kern<<<grid, kRegThreads, dyn, s>>>(A);                                            \
+        };                                                                                     \
+        if (unit) {                                                                            \
+            if (R == 16) go(k_cg_regwide<G_, 16, true, true, true>);                           \
+            else if (R == 24) go(k_cg_regwide<G_, 24, true, true, true>);                      \
+            else if (R == 32) go(k_cg_regwide<G_, 32, true, true, true>);                      \
+            else go(k_cg_regwide<G_, 44, true, true, true>);                                   \
+        } else {                                                                               \
+            if (R == 16) go(k_cg_regwide<G_, 16, false, true, true>);                          \
+            else if (R == 24) go(k_cg_regwide<G_, 24, false, true, true>);                     \
+            else if (R == 32) go(k_cg_regwide<G_, 32, false, true, true>);                     \
+            else go(k_cg_regwide<G_, 44, false, true, true>);                                  \
+        }                                                                                      \
     }
 
 }  // namespace gs

@@ -132,14 +132,17 @@ def chunked_er():
                                   "GSPARSE_REG_KEEP": "40"},
                                  {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_QR": "0"},
                                  {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_QR": "0", "GSPARSE_RES_UNIT": "0"},
-                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_QR": "0", "GSPARSE_REG_KEEP": "40"}],
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_QR": "0", "GSPARSE_REG_KEEP": "40"},
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_SPLIT": "2"},
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_SPLIT": "3"},
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_SPLIT": "4", "GSPARSE_RES_UNIT": "0"}],
                          ids=["m0", "m1", "m3", "m4", "m4-ell", "m4-q-global", "m4-7slots",
                               "m4-weighted-sell", "m4-weighted-ell", "m4-slices-global",
                               "m4-rb4w4", "m4-rb4w4-weighted", "m4-diag-loaded", "m4-w6", "m4-w8",
                               "m5", "m5-weighted", "m5-diag-loaded", "m5-7slots", "m5-p-global",
                               "m5-p-all-global-weighted", "m5-narrow", "m5-narrow-weighted",
                               "m5-narrow-p-global", "m5-q-recomputed", "m5-q-recomputed-weighted",
-                              "m5-q-recomputed-p-global"])
+                              "m5-q-recomputed-p-global", "m5-split2", "m5-split3", "m5-split4-weighted"])
 @pytest.mark.parametrize("threads", [3, 8])
 @pytest.mark.parametrize("graph", ["unit", "dup", "hub"])
 def test_approx_er_blas_chunks_vs_oracle(gs, chunked_er, graph, threads, env, monkeypatch):
@@ -154,11 +157,15 @@ def test_approx_er_blas_chunks_vs_oracle(gs, chunked_er, graph, threads, env, mo
     assert bits_equal(er, ref[threads])
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "3", "4", "5"])
+@pytest.mark.parametrize("mode", ["0", "1", "3", "4", "5", "5s"])
 def test_er_column_blocks_in_every_mode(gs, chunked_er, mode, monkeypatch):
     """A rank's column block [col0, col1) (the N-GPU split) solved alone, in the
     batched and the resident solver: the blocks' partial sums, added along the
-    pairwise tree, equal the whole -- and the whole equals the oracle."""
+    pairwise tree, equal the whole -- and the whole equals the oracle (5s: every
+    column solved by 2 workgroups, k_cg_regwide's split form)."""
+    if mode == "5s":
+        mode = "5"
+        monkeypatch.setenv("GSPARSE_REG_SPLIT", "2")
     monkeypatch.setenv("GSPARSE_CG_MODE", mode)
     n, graphs_ = chunked_er
     ei, ref = graphs_["unit"]
