@@ -241,7 +241,7 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
         }
     }
     const int64_t wslots = P ? std::min<int64_t>(ncu, std::max<int64_t>(W, 1)) : slots;
-    double *pg = (double *)c->buf("er_reg_pg").ensure(sizeof(double) * (size_t)std::max<int64_t>(wslots, 1) * ldn);
+    double *pg = (double *)c->buf("er_reg_pg").ensure(sizeof(double) * (size_t)std::max<int64_t>(std::max<int64_t>(wslots, slots), 1) * ldn);
     A.ld = ld;
     A.ldn = ldn;
     A.col0 = col0;
@@ -342,6 +342,8 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     B.xch = xch;
     B.flags = flg;
     B.abortf = flg + (size_t)groups * P;
+    B.spinmax = 1 << 22;  // polls before a hand-off gives up (a few seconds)
+    if (const char *e = getenv("GSPARSE_REG_SPLIT_SPIN")) B.spinmax = atoi(e);
     const unsigned grid = (unsigned)(groups * P);
     if (Gs == 4) regwide_split_launch_g4(B, Rs, ufast, dyns, grid, s);
     else regwide_split_launch_g8(B, Rs, ufast, dyns, grid, s);
@@ -349,7 +351,22 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     int32_t aborted = 0;
     GS_HIP(hipMemcpyAsync(&aborted, B.abortf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     GS_HIP(hipStreamSynchronize(s));
-    GS_CHECK(!aborted, GS_EHIP, "split CG: a hand-off between the %d parts of a column timed out", P);
+    if (aborted) {
+        // the parts of a column could not all be resident at once (another process or
+        // stream held CUs): solve the tail columns again, whole, one workgroup each
+        fprintf(stderr, "[gsparse] split CG hand-off timed out (%d parts); tail re-solved whole\n", P);
+        RegArgs Cw = A;
+        Cw.col0 = col0 + W;
+        Cw.ncols = tailn;
+        Cw.Xc = Xc + W * ldn;
+        Cw.prof = nullptr;
+        const int64_t ts = std::min<int64_t>(tailn, wslots > 1 ? wslots : slots);
+        if (G == 1) regwide_launch_g1(Cw, rsel, ufast, dyn, (unsigned)ts, s);
+        else if (G == 2) regwide_launch_g2(Cw, rsel, ufast, dyn, (unsigned)ts, s);
+        else if (G == 4) regwide_launch_g4(Cw, rsel, ufast, dyn, (unsigned)ts, s);
+        else regwide_launch_g8(Cw, rsel, ufast, dyn, (unsigned)ts, s);
+        GS_HIP(hipGetLastError());
+    }
 }
 
 }  // namespace gs

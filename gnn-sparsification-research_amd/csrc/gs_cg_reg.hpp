@@ -68,6 +68,7 @@ struct RegArgs {
     double *xch;          // [groups][2][kRegMaxChunks] chunk dots by hand-off parity
     int32_t *flags;       // [groups][P] hand-off sequence numbers (zeroed before the launch)
     int32_t *abortf;      // set when a hand-off poll gave up
+    int32_t spinmax;      // polls before it gives up
 };
 static constexpr int kRegPartTab = 4 * kRegMaxChunks + 4;
 
@@ -581,7 +582,7 @@ GS_REGWIDE_LAUNCH_DECL(2)
 GS_REGWIDE_LAUNCH_DECL(4)
 GS_REGWIDE_LAUNCH_DECL(8)
 #undef GS_REGWIDE_LAUNCH_DECL
-// split form, 4 or 8 threads per chain (gs_cg_reg_g4.hip, gs_cg_reg_g8.hip)
+// split form, 4 or 8 threads per chain (gs_cg_reg_s4.hip, gs_cg_reg_s8.hip)
 void regwide_split_launch_g4(const RegArgs &A, int R, bool unit, size_t dyn, unsigned grid, hipStream_t s);
 void regwide_split_launch_g8(const RegArgs &A, int R, bool unit, size_t dyn, unsigned grid, hipStream_t s);
 

@@ -6,5 +6,4 @@
 namespace gs {
 GS_REGRES_LAUNCH_DEF(4)
 GS_REGWIDE_LAUNCH_DEF(4)
-GS_REGWIDE_SPLIT_DEF(4)
 }  // namespace gs

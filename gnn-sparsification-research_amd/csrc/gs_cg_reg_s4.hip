@@ -1,0 +1,9 @@
+// gs_cg_reg_s4.hip -- instantiations of the split form of k_cg_regwide (q in registers,
+// P workgroups per column) with 4 threads per chain (gs_cg_wide.hpp); a file of its
+// own so it builds in parallel with gs_cg_reg_g4.hip.
+#include "gs_cg_reg.hpp"
+#include "gs_cg_wide.hpp"
+
+namespace gs {
+GS_REGWIDE_SPLIT_DEF(4)
+}  // namespace gs

@@ -314,7 +314,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                 if (q == part) continue;
                 for (int spin = 0; __hip_atomic_load(gflags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hseq;
                      ++spin) {
-                    if (spin > (1 << 22)) {
+                    if (spin >= A.spinmax) {
                         verdict = 1;
                         __hip_atomic_store(A.abortf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;

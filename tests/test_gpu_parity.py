@@ -135,14 +135,16 @@ def chunked_er():
                                  {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_QR": "0", "GSPARSE_REG_KEEP": "40"},
                                  {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_SPLIT": "2"},
                                  {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_SPLIT": "3"},
-                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_SPLIT": "4", "GSPARSE_RES_UNIT": "0"}],
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_SPLIT": "4", "GSPARSE_RES_UNIT": "0"},
+                                 {"GSPARSE_CG_MODE": "5", "GSPARSE_REG_SPLIT": "2", "GSPARSE_REG_SPLIT_SPIN": "0"}],
                          ids=["m0", "m1", "m3", "m4", "m4-ell", "m4-q-global", "m4-7slots",
                               "m4-weighted-sell", "m4-weighted-ell", "m4-slices-global",
                               "m4-rb4w4", "m4-rb4w4-weighted", "m4-diag-loaded", "m4-w6", "m4-w8",
                               "m5", "m5-weighted", "m5-diag-loaded", "m5-7slots", "m5-p-global",
                               "m5-p-all-global-weighted", "m5-narrow", "m5-narrow-weighted",
                               "m5-narrow-p-global", "m5-q-recomputed", "m5-q-recomputed-weighted",
-                              "m5-q-recomputed-p-global", "m5-split2", "m5-split3", "m5-split4-weighted"])
+                              "m5-q-recomputed-p-global", "m5-split2", "m5-split3", "m5-split4-weighted",
+                              "m5-split2-gives-up"])
 @pytest.mark.parametrize("threads", [3, 8])
 @pytest.mark.parametrize("graph", ["unit", "dup", "hub"])
 def test_approx_er_blas_chunks_vs_oracle(gs, chunked_er, graph, threads, env, monkeypatch):
