@@ -267,7 +267,10 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     A.ck = dch + 2 * kRegMaxChunks;
     A.cb = dch + 3 * kRegMaxChunks;
     A.prof = prof;
-    if (W > 0) {
+    // the whole-column launch (the first W columns); with a split tail it is issued
+    // after the tail's tables and ELL are prepared, so the split launch follows it at once
+    auto launch_whole = [&]() {
+        if (W <= 0) return;
         if (NT == 512) {
             if (G == 1) regwide_launch_g1(A, rsel, ufast, dyn, (unsigned)wslots, s);
             else if (G == 2) regwide_launch_g2(A, rsel, ufast, dyn, (unsigned)wslots, s);
@@ -278,8 +281,11 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
         else if (G == 4) regres_launch_g4(A, rsel, ufast, dyn, (unsigned)wslots, s);
         else regres_launch_g8(A, rsel, ufast, dyn, (unsigned)wslots, s);
         GS_HIP(hipGetLastError());
+    };
+    if (P < 2) {
+        launch_whole();
+        return;
     }
-    if (P < 2) return;
 
     // split tail: per-part chunk tables (LDS layout: the part's rows from slot 0, then
     // the zero slot) and an ELL whose codes each row's part resolves
@@ -308,8 +314,9 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     }
     auto *dpt = (int32_t *)c->buf("er_reg_split_ptab").ensure(sizeof(hpt));
     auto *dtab = (int64_t *)c->buf("er_reg_split_tab").ensure(sizeof(htab));
-    GS_HIP(hipMemcpy(dpt, hpt, sizeof(hpt), hipMemcpyHostToDevice));
-    GS_HIP(hipMemcpy(dtab, htab, sizeof(htab), hipMemcpyHostToDevice));
+    // stream-ordered copies; hpt / htab outlive them (the stream is synchronised below)
+    GS_HIP(hipMemcpyAsync(dpt, hpt, sizeof(hpt), hipMemcpyHostToDevice, s));
+    GS_HIP(hipMemcpyAsync(dtab, htab, sizeof(htab), hipMemcpyHostToDevice, s));
     auto *ells = (uint4 *)c->buf("er_reg_split_ell").ensure(sizeof(uint4) * n);
     double *ellvs = ufast ? nullptr : (double *)c->buf("er_reg_split_ellv").ensure(sizeof(double) * 8 * n);
     auto *ocols = (uint16_t *)c->buf("er_reg_split_ocol").ensure(sizeof(uint16_t) * (nov + 1));
@@ -345,6 +352,7 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     B.spinmax = 1 << 22;  // polls before a hand-off gives up (a few seconds)
     if (const char *e = getenv("GSPARSE_REG_SPLIT_SPIN")) B.spinmax = atoi(e);
     const unsigned grid = (unsigned)(groups * P);
+    launch_whole();
     if (Gs == 4) regwide_split_launch_g4(B, Rs, ufast, dyns, grid, s);
     else regwide_split_launch_g8(B, Rs, ufast, dyns, grid, s);
     GS_HIP(hipGetLastError());
