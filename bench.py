@@ -77,9 +77,10 @@ def pmc_traffic(name: str, workload: str):
     def kb(v):
         return (2.0 * v["FETCH_SIZE_KB_per_launch"] + v["WRITE_SIZE_KB_per_launch"]) * 1024.0
 
-    if name in ("jaccard", "metric_backbone"):
-        # pipelines: the kernels of one call summed (the plan / search kernel runs once per call)
-        anchor = "k_jac_plan" if name == "jaccard" else "k_bb_keep"
+    if name in ("jaccard", "metric_backbone", "cg_reg"):
+        # pipelines: the kernels of one call summed (the plan / search kernel runs once per
+        # call; cg_reg: the whole-column launch and the split launch of the last round)
+        anchor = {"jaccard": "k_jac_plan", "metric_backbone": "k_bb_keep", "cg_reg": "k_cg_reg"}[name]
         calls = max(1, max(v.get("launches", 1) for k, v in hits if anchor in k) if any(
             anchor in k for k, _ in hits) else 1)
         b = sum(kb(v) * v.get("launches", 1) for _, v in hits) / calls
