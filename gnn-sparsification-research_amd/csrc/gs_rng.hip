@@ -18,7 +18,6 @@
 
 namespace gs {
 
-static constexpr int kZigBlock = 1024;
 static constexpr int kZigEntries = 64;
 
 struct ZigTables {
@@ -33,7 +32,7 @@ struct ZigTables {
     int32_t *flags;   // [0]: #pending, [1]: overflow
 };
 
-__global__ void __launch_bounds__(64) k_zig_scan(u128 s0, u128 inc, int64_t nblk, ZigTables T) {
+__global__ void __launch_bounds__(64) k_zig_scan(u128 s0, u128 inc, int64_t nblk, int kZigBlock, ZigTables T) {
     int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (t >= nblk) return;
     const u128 st = pcg_advance(s0, inc, (uint64_t)t * kZigBlock);
@@ -133,18 +132,23 @@ __global__ void k_zig_select(int64_t nblk, ZigTables T) {
         T.sel[t] = T.cnt[t * kZigEntries + T.entry[t]];
 }
 
-__global__ void __launch_bounds__(64) k_zig_emit(u128 s0, u128 inc, int64_t nblk, ZigTables T,
-                                                 int64_t need, double *__restrict__ out) {
-    int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (t >= nblk) return;
-    int64_t idx = T.base[t];
+// one thread per span of ge consecutive parse blocks (1,024 draws): the parse from the
+// span's first entry runs straight through the later blocks' entries (the stream is
+// deterministic), so the normals come out in order from the span's first index
+__global__ void __launch_bounds__(64) k_zig_emit(u128 s0, u128 inc, int64_t nblk, int kZigBlock, int ge,
+                                                 ZigTables T, int64_t need, double *__restrict__ out) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t b0 = t * ge;
+    if (b0 >= nblk) return;
+    int64_t idx = T.base[b0];
     if (idx >= need) return;
-    const int e = T.entry[t];
-    Pcg64 g{pcg_advance(s0, inc, (uint64_t)t * kZigBlock + e), inc};
+    const int e = T.entry[b0];
+    const int span = (int)((b0 + ge <= nblk ? ge : nblk - b0) * kZigBlock);
+    Pcg64 g{pcg_advance(s0, inc, (uint64_t)b0 * kZigBlock + e), inc};
     int pos = e;
     bool prod;
     double v;
-    while (pos < kZigBlock && idx < need) {
+    while (pos < span && idx < need) {
         pos += zig_attempt<true>(g, &prod, &v);
         if (prod) out[idx++] = v;
     }
@@ -169,6 +173,16 @@ extern "C" int gs_er_project_pcg64(gs_ctx *c, uint64_t state_hi, uint64_t state_
         const u128 inc = ((u128)inc_hi << 64) | inc_lo;
         double *raw = (double *)er.rawbuf.ensure(sizeof(double) * (size_t)need);
         hipEvent_t t0 = prof_begin(c);
+        // draws per parse block: 256 while that still leaves few waves per SIMD (Roman:
+        // 344 k scan threads instead of 86 k; the scan 1.37 -> 0.91 ms), 1,024 for long
+        // streams, where the per-block tables (384 B per block) would otherwise add a
+        // fifth to the bytes written.  The emit always walks 1,024-draw spans (256-draw
+        // spans made its scattered stores slower: 0.63 -> 1.07 ms)
+        int kZigBlock = need < ((int64_t)1 << 29) ? 256 : 1024;
+        if (const char *e = getenv("GSPARSE_ZIG_BLOCK")) {
+            const int v = atoi(e);
+            if (v == 256 || v == 512 || v == 1024) kZigBlock = v;
+        }
         // NumPy's ziggurat consumes 1.022 draws per normal on average (measured,
         // 2e6 normals); start with 4% headroom so one attempt suffices
         int64_t draws = need + need / 25 + 4 * (int64_t)kZigBlock;
@@ -185,7 +199,7 @@ extern "C" int gs_er_project_pcg64(gs_ctx *c, uint64_t state_hi, uint64_t state_
             T.pending = (int32_t *)c->buf("zig_pending").ensure(sizeof(int32_t) * nblk);
             T.flags = (int32_t *)c->buf("zig_flags").ensure(64);
             GS_HIP(hipMemsetAsync(T.flags, 0, 64, s));
-            k_zig_scan<<<(unsigned)((nblk + 63) / 64), 64, 0, s>>>(s0, inc, nblk, T);
+            k_zig_scan<<<(unsigned)((nblk + 63) / 64), 64, 0, s>>>(s0, inc, nblk, kZigBlock, T);
             k_zig_link<<<grid_for(nblk, 256, 4096), 256, 0, s>>>(nblk, T);
             k_zig_link_seq<<<1, 1, 0, s>>>(T);
             k_zig_select<<<grid_for(nblk, 256, 4096), 256, 0, s>>>(nblk, T);
@@ -203,7 +217,9 @@ extern "C" int gs_er_project_pcg64(gs_ctx *c, uint64_t state_hi, uint64_t state_
                 draws = draws + draws / 4;
                 continue;
             }
-            k_zig_emit<<<(unsigned)((nblk + 63) / 64), 64, 0, s>>>(s0, inc, nblk, T, need, raw);
+            const int ge = 1024 / kZigBlock;  // emit spans of 1,024 draws (fewer, longer store streams)
+            const int64_t nspan = (nblk + ge - 1) / ge;
+            k_zig_emit<<<(unsigned)((nspan + 63) / 64), 64, 0, s>>>(s0, inc, nblk, kZigBlock, ge, T, need, raw);
             GS_HIP(hipGetLastError());
             prof_end(c, t0, "er_rng", 8.0 * (double)need);
             // Y = B @ (R / sqrt(k)) over all m rows, straight from the device buffer
