@@ -186,6 +186,34 @@ def test_er_column_blocks_in_every_mode(gs, chunked_er, mode, monkeypatch):
     assert bits_equal(tot, ref[8])
 
 
+def test_split_tail_in_offset_column_blocks(gs, chunked_er, monkeypatch):
+    """Column blocks that start past column 0 and leave a split last round (each
+    block ~325 columns: one whole round of 256, then ~69 columns in 3 parts) give
+    the same bits as the whole solve with the split form disabled."""
+    monkeypatch.setenv("GSPARSE_CG_MODE", "5")
+    n, graphs_ = chunked_er
+    ei, _ = graphs_["unit"]
+    sp_ = gs.GraphSparsifier(gs.Data(edge_index=torch.from_numpy(ei), num_nodes=n), "cpu")
+    e = sp_._engine
+    k = gs.engine.jl_dim(n, 0.59)
+    e.er_prepare(k)
+    e.er_project_device(np.random.default_rng(42), k)
+    monkeypatch.setenv("GSPARSE_REG_SPLIT", "0")
+    e.er_solve(0, k, 40, 1e-6, 8)
+    whole = e.er_scores(0, k, finalize=False).copy()
+    monkeypatch.delenv("GSPARSE_REG_SPLIT")
+    b = gs.engine.er_split(k, 2)
+    assert 256 < int(b[1]) - int(b[0]) <= 384 and 256 < int(b[2]) - int(b[1]) <= 384
+    sums = []
+    for i in range(2):
+        e.er_solve(int(b[i]), int(b[i + 1]), 40, 1e-6, 8)
+        sums.append(e.er_scores(int(b[i]), int(b[i + 1]), finalize=False).copy())
+    e.er_solve(0, k, 40, 1e-6, 8)  # whole range, split tail on
+    assert bits_equal(e.er_scores(0, k, finalize=False), whole)
+    # the blocks' partial sums are pairwise-tree halves of the whole sum
+    assert bits_equal(0.0 + (sums[0] + sums[1]), whole)
+
+
 def test_approx_er_roman_full_bit_exact(gs):
     """configs[1] size (n=22,662, E=65,854, k=2,674, 500 CG iterations per column)."""
     g = load_golden("roman_full")
