@@ -40,9 +40,6 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# aggregate LDS read rate: ds_read_b64 moves 256 B/clk/CU (MI355X_MICROARCH.md, LDS table)
-# x 256 CUs x 2.4 GHz -- the on-chip bound of the register-resident CG solver
-LDS_PEAK_GBS = 256 * 256 * 2.4
 # MI355X dense fp64 matrix peak as AMD publishes it (the microarchitecture guide lists
 # no fp64 figure); a register-only v_mfma_f64_16x16x4_f64 loop sustains 49-50 on the
 # box (tools/mfma_f64_peak.hip, profiles/r01j_mfma_f64_peak.log).
@@ -56,55 +53,100 @@ PMC_KERNEL = {"cg_res": "gs::k_cg_resident<", "cg_reg": "gs::k_cg_reg", "cg_pq":
               "cg_p": "gs::k_cg_p", "cg_spmv": "gs::k_spmv<"}
 
 
-def pmc_traffic(name: str, workload: str):
-    """HBM bytes per launch of the dominant kernel from the newest committed
-    rocprofv3 --pmc summary of this workload (profiles/*_<workload>_pmc_summary.json,
-    made by tools/profile_bench.sh: separate FETCH_SIZE / WRITE_SIZE passes).
-    FETCH_SIZE counts 1/2 of a wide coalesced stream on gfx950 and is doubled,
-    WRITE_SIZE is exact (MI355X_MICROARCH.md, HBM section); both are KB."""
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from provenance import source_hash  # noqa: E402
+
+SRC_HASH = source_hash()
+CU_COUNT, CLOCK_GHZ = 256, 2.4  # MI355X (MI355X_MICROARCH.md): issue-rate peaks below
+
+
+def pmc_summary(workload: str):
+    """The newest committed rocprofv3 PMC summary of this workload
+    (profiles/*_<workload>_pmc_summary.json, tools/profile_bench.sh) that profiled
+    THIS tree's libgsparse sources (its _meta.source_hash); counters of other code
+    are never joined to this run's timings.  Returns (summary, file, note)."""
     import glob
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_pmc_summary.json")))
+    stale = None
+    for f in reversed(files):
+        with open(f) as fh:
+            summ = json.load(fh)
+        h = summ.get("_meta", {}).get("source_hash")
+        if h == SRC_HASH:
+            return summ, os.path.basename(f), None
+        stale = stale or f"newest summary {os.path.basename(f)} profiled sources {h}, not {SRC_HASH}"
+    return None, None, stale or f"no PMC summary of workload {workload!r}"
+
+
+def kernel_counters(summ: dict, name: str):
+    """Per-call counters of profiler entry `name`: the kernels of one call summed
+    (pipelines: the plan kernel or the whole-column launch runs once per call)."""
     pre = PMC_KERNEL.get(name)
-    if not files or pre is None:
-        return None, None
-    with open(files[-1]) as fh:
-        summ = json.load(fh)
-    hits = [(k, v) for k, v in summ.items() if k.startswith("void " + pre) or k.startswith(pre)]
-    hits = [(k, v) for k, v in hits if "FETCH_SIZE_KB_per_launch" in v and "WRITE_SIZE_KB_per_launch" in v]
+    if not summ or pre is None:
+        return None
+    hits = [(k, v) for k, v in summ.items()
+            if k != "_meta" and (k.startswith("void " + pre) or k.startswith(pre))]
     if not hits:
-        return None, None
-    def kb(v):
-        return (2.0 * v["FETCH_SIZE_KB_per_launch"] + v["WRITE_SIZE_KB_per_launch"]) * 1024.0
+        return None
+    anchor = {"jaccard": "k_jac_plan", "metric_backbone": "k_bb_keep", "cg_reg": "k_cg_reg"}.get(name)
+    if anchor and any(anchor in k for k, _ in hits):
+        calls = max(1, max(v.get("launches", 1) for k, v in hits if anchor in k))
+    else:
+        hits = [max(hits, key=lambda kv: kv[1].get("launches", 0))]
+        calls = hits[0][1].get("launches", 1)
+    out = {}
+    for _, v in hits:
+        for c, x in v.items():
+            if c.endswith("_per_launch"):
+                out[c[: -len("_per_launch")]] = out.get(c[: -len("_per_launch")], 0.0) + \
+                    x * v.get("launches", 1) / calls
+    out["kernels"] = len(hits)
+    return out
 
-    if name in ("jaccard", "metric_backbone", "cg_reg"):
-        # pipelines: the kernels of one call summed (the plan / search kernel runs once per
-        # call; cg_reg: the whole-column launch and the split launch of the last round)
-        anchor = {"jaccard": "k_jac_plan", "metric_backbone": "k_bb_keep", "cg_reg": "k_cg_reg"}[name]
-        calls = max(1, max(v.get("launches", 1) for k, v in hits if anchor in k) if any(
-            anchor in k for k, _ in hits) else 1)
-        b = sum(kb(v) * v.get("launches", 1) for _, v in hits) / calls
-        return b, f"{os.path.basename(files[-1])}: sum of {len(hits)} {pre}* kernels"
-    k, v = max(hits, key=lambda kv: kv[1].get("launches", 0))
-    return kb(v), f"{os.path.basename(files[-1])}: {k}"
 
-
-def add_traffic(roofline: dict, traffic, tsrc, avg_ms: float) -> dict:
-    """Label both fractions.  ``frac`` stays achieved / peak with achieved from
-    the ALGORITHMIC bytes (the bench contract; above 1 when the working set is
-    re-read from the Infinity Cache / L2 instead of HBM).  When a rocprofv3 PMC
-    summary exists, ``traffic_gbps`` / ``traffic_frac`` are the measured fabric
-    bytes (2 x FETCH_SIZE + WRITE_SIZE, per launch) over the same launch time --
-    the counter-based bound of what actually left the L2."""
-    roofline["frac_basis"] = "algorithmic bytes (SURVEY 8(d))"
-    roofline["traffic"] = round(traffic) if traffic else None
-    if traffic and avg_ms > 0:
-        gbps = traffic / (avg_ms * 1e-3) / 1e9
-        roofline["traffic_gbps"] = round(gbps, 1)
-        roofline["traffic_frac"] = round(gbps / HBM_PEAK_GBS, 4)
-    if tsrc:
-        roofline["traffic_source"] = tsrc
-    return roofline
+def make_roofline(name: str, avg_ms: float, bytes_per: float, launches: int, workload: str,
+                  world: int) -> dict:
+    """Roofline of the dominant kernel.  Headline (`achieved`, `frac`): measured
+    HBM-side traffic -- rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per call of the same
+    sources (FETCH_SIZE counts half of a wide stream on gfx950, WRITE_SIZE is exact:
+    MI355X_MICROARCH.md) -- over this run's HIP-event launch time; a bound the
+    kernel can reach.  `algorithmic`: SURVEY 8(d)'s bytes over the same time (above
+    1 when the working set is re-read from LDS, registers or the Infinity Cache
+    instead of HBM).  `on_chip`: issue rates from the SQ counters of the same
+    summary (LDS / VALU instructions per CU-cycle, wave time spent waiting)."""
+    alg = bytes_per / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    roof = {"kernel": name, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": None, "traffic": None, "avg_launch_ms": round(avg_ms, 5), "launches": launches,
+            "basis": "measured traffic: rocprofv3 (2 x FETCH_SIZE + WRITE_SIZE) per call, same "
+                     "sources, / live HIP-event launch time",
+            "algorithmic": {"bytes_per_launch": bytes_per, "achieved": round(alg, 1),
+                            "frac": round(alg / HBM_PEAK_GBS, 4),
+                            "note": "SURVEY 8(d) algorithmic bytes; may exceed 1 (reuse on chip)"}}
+    if world > 1:  # the committed summaries are of 1-GPU runs (a rank launches a share)
+        roof["basis"] = "no PMC at N > 1 (summaries are 1-GPU runs); see algorithmic"
+        return roof
+    summ, src, note = pmc_summary(workload)
+    ctr = kernel_counters(summ, name) if summ else None
+    if ctr is None or "FETCH_SIZE_KB" not in ctr or "WRITE_SIZE_KB" not in ctr:
+        roof["basis"] = f"no counters for {name}: {note or src}; see algorithmic"
+        return roof
+    traffic = (2.0 * ctr["FETCH_SIZE_KB"] + ctr["WRITE_SIZE_KB"]) * 1024.0
+    gbps = traffic / (avg_ms * 1e-3) / 1e9
+    roof.update(achieved=round(gbps, 1), frac=round(gbps / HBM_PEAK_GBS, 4), traffic=round(traffic),
+                traffic_source=f"{src} ({ctr['kernels']} kernel(s) per call)")
+    cyc = avg_ms * 1e-3 * CLOCK_GHZ * 1e9 * CU_COUNT  # CU-cycles of one launch
+    oc = {}
+    if "SQ_INSTS_LDS" in ctr:
+        oc["lds_issue_frac"] = round(ctr["SQ_INSTS_LDS"] / cyc, 4)  # <= 1 LDS instruction / CU / clk
+    if "SQ_INSTS_VALU" in ctr:
+        oc["valu_issue_frac"] = round(ctr["SQ_INSTS_VALU"] / (4 * cyc), 4)  # 4 SIMDs per CU
+    if "SQ_WAIT_ANY" in ctr and ctr.get("SQ_WAVE_CYCLES"):
+        oc["wave_wait_frac"] = round(ctr["SQ_WAIT_ANY"] / ctr["SQ_WAVE_CYCLES"], 4)
+    if oc:
+        oc["source"] = src
+        roof["on_chip"] = oc
+    return roof
 
 
 def log(*a):
@@ -132,13 +174,27 @@ def emit(result):
     print(json.dumps(result), flush=True)
 
 
-def cpu_baseline_roman(ei, n, sample_cols, threads):
+def host_cores() -> int:
+    """CPU threads this process is granted: $OMP_NUM_THREADS when set (the GPU box
+    sets it to its share of the host, 16 of 256), capped at the affinity mask."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(env))) if env and env.isdigit() else aff
+
+
+def cpu_baseline_roman(ei, n, sample_cols, threads, all_cores_cols=16):
     """The reference algorithm restated with identical NumPy/SciPy calls
     (oracle/gsparse_oracle.py), timed on a bounded sample of the same
     workload: full Jaccard (A@A + gather, metrics.py:43-62), full R stream and
     Y = B @ R (metrics.py:272-275), SciPy CG on `sample_cols` of the k columns
     (metrics.py:284-289) extrapolated by k/sample_cols, and the diff^2 row sums
-    (metrics.py:292-293) extrapolated from 64 columns."""
+    (metrics.py:292-293) extrapolated from 64 columns.  The headline uses
+    `threads` OpenBLAS threads (1: the fastest for this CG); the same pipeline
+    with every core this process may use is reported beside it (`all_cores`,
+    CG on `all_cores_cols` columns)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import scipy.sparse as sp
     import scipy.sparse.linalg as spla
@@ -148,70 +204,107 @@ def cpu_baseline_roman(ei, n, sample_cols, threads):
 
     ip, ix, d = O.canonical_csr(ei, n)
     adj = sp.csr_matrix((d, ix, ip), shape=(n, n))
-    with threadpool_limits(limits=threads, user_api="blas"):
-        t0 = time.perf_counter()
-        ab = (adj > 0).astype(np.float64)
-        deg = np.asarray(ab.sum(axis=1)).flatten()
-        inter = ab @ ab
-        rows, cols = ab.nonzero()
-        ic = np.asarray(inter[rows, cols]).flatten()
-        uni = deg[rows] + deg[cols] - ic
-        _ = np.divide(ic, uni, out=np.zeros_like(ic), where=uni > 0)
-        t_jac = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        Y, m, kk = O.approx_er_projection(ip, ix, n)
-        L = O.laplacian_reg(ip, ix, d, n)
-        t_proj = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        for i in range(sample_cols):
-            spla.cg(L, Y[:, i], maxiter=500, rtol=1e-6)
-        t_cg = (time.perf_counter() - t0) * kk / sample_cols
-        t0 = time.perf_counter()
-        Z = np.zeros((n, 64))
-        diff = Z[rows] - Z[cols]
-        _ = np.sum(diff ** 2, axis=1)
-        t_fin = (time.perf_counter() - t0) * kk / 64
-    total = t_jac + t_proj + t_cg + t_fin
-    return {
-        "value": float(len(ix) / total),
-        "unit": "scored edges/s",
-        "cores": int(threads),
-        "kind": "port",
-        "sample": (f"full Jaccard ({t_jac:.3f}s) + full R/Y projection ({t_proj:.2f}s) + SciPy CG "
-                   f"on {sample_cols}/{kk} columns x500 iters extrapolated ({t_cg:.1f}s) + "
-                   f"diff^2 sum extrapolated ({t_fin:.2f}s); OpenBLAS threads={threads}"),
-        "seconds_extrapolated": round(total, 3),
-    }
+
+    def run(th, cols):
+        with threadpool_limits(limits=th, user_api="blas"):
+            t0 = time.perf_counter()
+            ab = (adj > 0).astype(np.float64)
+            deg = np.asarray(ab.sum(axis=1)).flatten()
+            inter = ab @ ab
+            rows, cols_ = ab.nonzero()
+            ic = np.asarray(inter[rows, cols_]).flatten()
+            uni = deg[rows] + deg[cols_] - ic
+            _ = np.divide(ic, uni, out=np.zeros_like(ic), where=uni > 0)
+            t_jac = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            Y, m, kk = O.approx_er_projection(ip, ix, n)
+            L = O.laplacian_reg(ip, ix, d, n)
+            t_proj = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            for i in range(cols):
+                spla.cg(L, Y[:, i], maxiter=500, rtol=1e-6)
+            t_cg = (time.perf_counter() - t0) * kk / cols
+            t0 = time.perf_counter()
+            Z = np.zeros((n, 64))
+            diff = Z[rows] - Z[cols_]
+            _ = np.sum(diff ** 2, axis=1)
+            t_fin = (time.perf_counter() - t0) * kk / 64
+        total = t_jac + t_proj + t_cg + t_fin
+        return total, (f"full Jaccard ({t_jac:.3f}s) + full R/Y projection ({t_proj:.2f}s) + SciPy CG "
+                       f"on {cols}/{kk} columns x500 iters extrapolated ({t_cg:.1f}s) + "
+                       f"diff^2 sum extrapolated ({t_fin:.2f}s); OpenBLAS threads={th}")
+
+    total, sample = run(threads, sample_cols)
+    res = {"value": float(len(ix) / total), "unit": "scored edges/s", "cores": int(threads),
+           "kind": "port", "sample": sample, "seconds_extrapolated": round(total, 3)}
+    allc = host_cores()
+    if allc > threads:
+        t_all, s_all = run(allc, all_cores_cols)
+        res["all_cores"] = {"value": float(len(ix) / t_all), "cores": allc, "sample": s_all,
+                            "seconds_extrapolated": round(t_all, 3)}
+    return res
 
 
-def cpu_baseline_jaccard(ei, n, threads, max_edges=2_000_000):
-    """Reference-style SpGEMM Jaccard (metrics.py:43-62) on a row-prefix sample."""
+def cpu_baseline_rmat(ip, ix, n, scale, merge_steps=3e9, spgemm_scale=15):
+    """configs[3] CPU baseline, two legs on this host's cores (1 thread each):
+    (1) the per-edge sorted-list merge restated in C (oracle.c, the same counts and
+    division as metrics.py:43-62) on the rows of a prefix holding ~merge_steps merge
+    steps, extrapolated by the whole graph's sum of (d_u + d_v);
+    (2) the reference's own SpGEMM Jaccard (A_bin @ A_bin, gather, divide:
+    metrics.py:43-62) on the full R-MAT-`spgemm_scale` graph -- the largest that
+    runs in ~15 s here (R-MAT-22 would materialise ~1e11 two-hop pairs) --
+    extrapolated to this graph by the SpGEMM's work sum_w d_w^2."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes
+
     import scipy.sparse as sp
     from threadpoolctl import threadpool_limits
 
     import gsparse_oracle as O
+    from gsparse import graphs
 
-    ip, ix, d = O.canonical_csr(ei, n)
-    rows_cut = int(np.searchsorted(ip, min(max_edges, len(ix))))
-    sub = sp.csr_matrix((d[: ip[rows_cut]], ix[: ip[rows_cut]], ip[: rows_cut + 1]),
-                        shape=(rows_cut, n))
-    adj = sp.csr_matrix((d, ix, ip), shape=(n, n))
-    with threadpool_limits(limits=threads, user_api="blas"):
+    deg = np.diff(ip)
+    rows = np.repeat(np.arange(n, dtype=np.int64), deg)
+    work = deg[rows] + deg[ix]
+    cw = np.cumsum(np.bincount(rows, weights=work, minlength=n))
+    r1 = int(min(n, np.searchsorted(cw, merge_steps) + 1))
+    tp, ti = O.transpose(ip, ix, n)
+    out = np.zeros(len(ix), dtype=np.float64)
+    t0 = time.perf_counter()
+    O.lib().oracle_jaccard_rows(O._p(ip, O._i64p), O._p(ix, O._i32p), O._p(tp, O._i64p),
+                                O._p(ti, O._i32p), ctypes.c_int64(0), ctypes.c_int64(r1),
+                                O._p(out, O._f64p))
+    t_merge = time.perf_counter() - t0
+    frac = float(cw[r1 - 1]) / float(cw[-1])
+    merge_total = t_merge / frac
+    # (2) reference SpGEMM on a smaller R-MAT, scaled by sum_w d_w^2
+    ei_s = graphs.rmat(spgemm_scale, 8, seed=0)
+    ns = 1 << spgemm_scale
+    ips, ixs, ds = O.canonical_csr(ei_s, ns)
+    adj = sp.csr_matrix((ds, ixs, ips), shape=(ns, ns))
+    with threadpool_limits(limits=1, user_api="blas"):
         t0 = time.perf_counter()
-        ab = (sub > 0).astype(np.float64)
-        full = (adj > 0).astype(np.float64)
-        deg = np.asarray(full.sum(axis=1)).flatten()
-        inter = ab @ full
-        rows, cols = ab.nonzero()
-        ic = np.asarray(inter[rows, cols]).flatten()
-        uni = deg[rows] + deg[cols] - ic
+        ab = (adj > 0).astype(np.float64)
+        dg = np.asarray(ab.sum(axis=1)).flatten()
+        inter = ab @ ab
+        rr, cc = ab.nonzero()
+        ic = np.asarray(inter[rr, cc]).flatten()
+        uni = dg[rr] + dg[cc] - ic
         _ = np.divide(ic, uni, out=np.zeros_like(ic), where=uni > 0)
-        t = time.perf_counter() - t0
-    return {"value": float(len(rows) / t), "unit": "scored edges/s", "cores": int(threads),
-            "kind": "port",
-            "sample": f"reference-style SpGEMM Jaccard on the first {len(rows)} CSR edges "
-                      f"({t:.2f}s); OpenBLAS threads={threads}"}
+        t_sp = time.perf_counter() - t0
+    w_small = float(np.sum(np.diff(ips).astype(np.float64) ** 2))
+    w_big = float(np.sum(deg.astype(np.float64) ** 2))
+    spgemm_total = t_sp * w_big / w_small
+    best = min(merge_total, spgemm_total)
+    return {"value": float(len(ix) / best), "unit": "scored edges/s", "cores": 1, "kind": "port",
+            "sample": (f"per-edge merge (oracle.c) on rows [0, {r1}) = {frac:.3%} of the merge steps: "
+                       f"{t_merge:.1f}s -> {merge_total:.0f}s for RMAT-{scale}; reference SpGEMM "
+                       f"(metrics.py:43-62) on the full RMAT-{spgemm_scale} ({len(ixs)} edges): "
+                       f"{t_sp:.1f}s -> {spgemm_total:.0f}s for RMAT-{scale} by sum d^2 "
+                       f"({w_big:.3g} / {w_small:.3g}); value = the faster leg"),
+            "seconds_extrapolated": round(best, 1),
+            "legs": {"merge_restated_s": round(merge_total, 1),
+                     "reference_spgemm_s": round(spgemm_total, 1)}}
 
 
 def cpu_baseline_backbone(ei, n, w, n_src=16, seed=0):
@@ -283,7 +376,7 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
                  w.numel(), GS_DEVICE, 1e-9, rank, world, keep.data_ptr(), GS_DEVICE,
                  ctypes.byref(relax))
         if comm is not None:
-            return comm.all_reduce_sum(keep.to(torch.int32))
+            return comm.all_reduce_sum(keep)
         return keep
 
     for _ in range(args.warmup):
@@ -313,17 +406,10 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
     roofline = None
     if prof and "metric_backbone" in prof:
         p = prof["metric_backbone"]
-        avg_ms = p["ms"] / p["launches"]
-        bytes_per = p["bytes"] / p["launches"]
-        achieved = bytes_per / (avg_ms * 1e-3) / 1e9
-        roofline = {"kernel": "metric_backbone", "bound": "hbm", "achieved": round(achieved, 1),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "avg_launch_ms": round(avg_ms, 3), "algorithmic_bytes_per_launch": bytes_per,
-                    "launches": p["launches"], "relaxations_per_launch_rank0": relax.value}
         key = f"backbone-{args.bb_graph}" + (str(args.bb_scale) if args.bb_graph == "rmat" else "")
-        traffic, tsrc = pmc_traffic("metric_backbone", key) if world == 1 else (None, None)
-        add_traffic(roofline, traffic, tsrc, avg_ms)
+        roofline = make_roofline("metric_backbone", p["ms"] / p["launches"], p["bytes"] / p["launches"],
+                                 p["launches"], key, world)
+        roofline["relaxations_per_launch_rank0"] = relax.value
     result = {
         "metric": "scored edges/sec (metric backbone)", "value": round(E * args.steps / elapsed, 1),
         "unit": "scored edges/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -707,15 +793,8 @@ def bench_scorers(args, world, rank, local_rank, dev, dist):
     name = next((kk for kk in ("cg_reg", "cg_res") if kk in prof), None) or max(
         prof, key=lambda kk: prof[kk]["ms"])
     p = prof[name]
-    avg_ms = p["ms"] / p["launches"]
-    achieved = p["bytes"] / p["launches"] / (avg_ms * 1e-3) / 1e9
-    traffic, tsrc = pmc_traffic(name, "roman") if world == 1 else (None, None)
-    roofline = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "avg_launch_ms": round(avg_ms, 5),
-                "algorithmic_bytes_per_launch": p["bytes"] / p["launches"],
-                "launches": p["launches"]}
-    add_traffic(roofline, traffic, tsrc, avg_ms)
+    roofline = make_roofline(name, p["ms"] / p["launches"], p["bytes"] / p["launches"], p["launches"],
+                             "roman", world)
     result = {
         "metric": "scored edges/sec (Jaccard+AA+FeatCos+ApproxER)",
         "value": round(world * E * args.steps / elapsed, 1), "unit": "scored edges/s",
@@ -750,6 +829,48 @@ def bench_scorers(args, world, rank, local_rank, dev, dist):
         emit(result)
 
 
+def spawn_ranks(n: int, rehearse: bool) -> None:
+    """`bench.py --gpus N` without a launcher: start N ranks (one per GPU) with
+    torch.distributed.run as a child process and exit with its status -- the
+    driver's own launch (torchrun + WORLD_SIZE) skips this.  Fails loudly when
+    fewer than N GPUs are visible (GSPARSE_REHEARSE=1: ranks share them)."""
+    import socket
+    import subprocess
+
+    visible = torch.cuda.device_count()
+    if n > visible and not rehearse:
+        raise SystemExit(f"bench.py: --gpus {n} needs {n} GPUs, {visible} visible")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    log(f"bench.py: launching {n} ranks: {' '.join(cmd)}")
+    sys.exit(subprocess.call(cmd))
+
+
+def check_ranks(dist, world: int, local_rank: int, rehearse: bool) -> None:
+    """Every rank is up, and (unless rehearsing) each drives its own GPU."""
+    props = torch.cuda.get_device_properties(local_rank)
+    ident = (socket_host(), str(getattr(props, "uuid", "")) or str(local_rank),
+             getattr(props, "pci_bus_id", None), local_rank)
+    seen = [None] * world
+    dist.all_gather_object(seen, ident)
+    assert len(seen) == world, seen
+    if not rehearse:
+        devs = {(h, u, b) for h, u, b, _ in seen}
+        if len(devs) != world:
+            raise SystemExit(f"bench.py: {world} ranks share GPUs: {seen}")
+
+
+def socket_host() -> str:
+    import socket
+
+    return socket.gethostname()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -770,20 +891,36 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    rehearse = os.environ.get("GSPARSE_REHEARSE") == "1"
+    if rehearse:
+        # ranks sharing a GPU cannot keep every part of a split CG column resident
+        os.environ.setdefault("GSPARSE_REG_SPLIT", "0")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: start the ranks before this process touches the GPU
+        # (torch.cuda.device_count() does not initialise HIP on this image)
+        return spawn_ranks(args.gpus, rehearse)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    # one process per GPU; modulo the visible count so a 1-GPU box can rehearse N>1
-    local_rank = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    visible = torch.cuda.device_count()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if local_rank >= visible:
+        if not rehearse:
+            raise SystemExit(f"bench.py: LOCAL_RANK {local_rank} but only {visible} GPU(s) visible "
+                             "(GSPARSE_REHEARSE=1 shares them, for rehearsals only)")
+        local_rank %= max(1, visible)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local_rank)
-        backend = os.environ.get("GSPARSE_DIST_BACKEND", "nccl")
+        backend = os.environ.get("GSPARSE_DIST_BACKEND", "gloo" if rehearse else "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(backend)
+        check_ranks(dist, world, local_rank, rehearse)
     dev = torch.device("cuda", local_rank)
 
     from gsparse import graphs
@@ -826,13 +963,13 @@ def main():
     nnz = eng.nnz
     k = jl_dim(n, 0.3)
     comm = Comm(device=dev) if world > 1 else None
-    bounds = None  # symmetric graphs: Jaccard shards by owner-side pair tasks (gs_jaccard_part)
+    bounds = None  # symmetric graphs: owner-pair count shares + all-gather (sharded_jaccard)
     jac_out = torch.empty(nnz, dtype=torch.float64, device=dev)
     er_out = torch.empty(nnz, dtype=torch.float64, device=dev)
 
     def step():
         if world > 1:
-            jac = sharded_edge_scores(eng, comm, "jaccard", bounds=bounds)
+            jac = sharded_edge_scores(eng, comm, "jaccard", bounds=bounds, out=jac_out)
             er = sharded_approx_er(eng, comm, blas_threads=args.blas_threads,
                                    rng_mode=args.rng) if with_er else None
             return jac, er
@@ -877,25 +1014,9 @@ def main():
     # roofline: the dominant kernel by summed time (HIP events on its stream)
     roofline = None
     if prof:
-        name, p = max(prof.items(), key=lambda kv: kv[1]["ms"])
-        avg_ms = p["ms"] / p["launches"]
-        bytes_per = p["bytes"] / p["launches"]
-        achieved = bytes_per / (avg_ms * 1e-3) / 1e9
-        # the committed PMC summaries are of 1-GPU runs (a rank at N > 1 launches a share)
-        traffic, tsrc = pmc_traffic(name, args.workload) if world == 1 else (None, None)
-        roofline = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "avg_launch_ms": round(avg_ms, 5),
-                    "algorithmic_bytes_per_launch": bytes_per, "launches": p["launches"]}
-        add_traffic(roofline, traffic, tsrc, avg_ms)
-        if name == "cg_reg":
-            # B_ER's bytes move through LDS and registers in this solver (p gathered from
-            # LDS, r / x / q in registers); against the LDS rate it is latency-bound, not
-            # bandwidth-bound (SQ counters)
-            roofline["on_chip"] = {"bound": "lds", "achieved": round(achieved, 1),
-                                   "peak": round(LDS_PEAK_GBS, 1), "unit": "GB/s",
-                                   "frac": round(achieved / LDS_PEAK_GBS, 4)}
+        name, p = max(((k, v) for k, v in prof.items() if v["ms"] > 0), key=lambda kv: kv[1]["ms"])
+        roofline = make_roofline(name, p["ms"] / p["launches"], p["bytes"] / p["launches"],
+                                 p["launches"], args.workload, world)
     kernels = {k2: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k2, v in prof.items()}
 
     result = {
@@ -925,7 +1046,8 @@ def main():
         if args.workload == "roman":
             result["cpu_baseline"] = cpu_baseline_roman(ei, n, args.cpu_sample_cols, 1)
         elif args.workload == "rmat":
-            result["cpu_baseline"] = cpu_baseline_jaccard(ei, n, 1)
+            ip_h, ix_h, _ = ctx.csr()
+            result["cpu_baseline"] = cpu_baseline_rmat(ip_h, ix_h, n, args.scale)
     if rank == 0:
         emit(result)
     if dist:

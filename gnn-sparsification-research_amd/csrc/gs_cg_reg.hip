@@ -125,16 +125,6 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     int NT = 0, G = 0, rsel = 0;
     GS_CHECK(reg_pick(n, T, hlen, NT, G, rsel), GS_EUNSUPPORTED,
              "register-resident CG: n=%lld, %d chunks out of range", (long long)n, T);
-    // ELL-8 copy (uint16 columns), overflow entries in CSR form
-    auto *ocnt = (int64_t *)c->buf("er_reg_ocnt").ensure(sizeof(int64_t) * (n + 1));
-    auto *optr = (int64_t *)c->buf("er_reg_optr").ensure(sizeof(int64_t) * (n + 1));
-    GS_HIP(hipMemsetAsync(ocnt, 0, sizeof(int64_t) * (n + 1), s));
-    auto *rlen = (uint16_t *)c->buf("er_reg_rlen").ensure(sizeof(uint16_t) * n);
-    k_ell8_count<<<grid_for(n, 256, 8192), 256, 0, s>>>((int32_t)n, lp, ocnt, rlen);
-    exclusive_scan_i64(c, ocnt, optr, n + 1);
-    int64_t nov = 0;
-    GS_HIP(hipMemcpyAsync(&nov, optr + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    GS_HIP(hipStreamSynchronize(s));
     // LDS: p (each chunk's LDS-resident prefix, in chunk order), the zero and scratch
     // slots, (one-wave form) 2 diagonal slots per thread, 6 x 32 T doubles of chain
     // sums / tail rows, the chunk table
@@ -161,30 +151,58 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     const uint32_t pad = (uint32_t)zs;  // the zero slot
     const size_t dyn =
         sizeof(double) * ((size_t)zs + 2 + dsl + 6 * (size_t)nch + 2 * kRegMaxChunks);
+    // ELL-8 copy (uint16 p codes), overflow entries in CSR form: rebuilt only when the
+    // graph, L_reg's shift or the chunk / LDS layout changed (the key)
+    double regv = c->er.reg;
+    int64_t regbits;
+    memcpy(&regbits, &regv, sizeof(regbits));
+    std::vector<int64_t> key = {c->g.epoch, regbits, n, T, G, NT, ufast ? 1 : 0, unit, dcount};
+    for (int t = 0; t < T; ++t) key.insert(key.end(), {ha[t], hlen[t], keep[t]});
+    auto *ocnt = (int64_t *)c->buf("er_reg_ocnt").ensure(sizeof(int64_t) * (n + 1));
+    auto *optr = (int64_t *)c->buf("er_reg_optr").ensure(sizeof(int64_t) * (n + 1));
+    auto *rlen = (uint16_t *)c->buf("er_reg_rlen").ensure(sizeof(uint16_t) * n);
+    const bool fresh = key != c->reg_ell_key;
+    if (fresh) {
+        c->reg_ell_key.clear();
+        c->reg_split_key.clear();
+        GS_HIP(hipMemsetAsync(ocnt, 0, sizeof(int64_t) * (n + 1), s));
+        k_ell8_count<<<grid_for(n, 256, 8192), 256, 0, s>>>((int32_t)n, lp, ocnt, rlen);
+        exclusive_scan_i64(c, ocnt, optr, n + 1);
+        GS_HIP(hipMemcpyAsync(&c->reg_nov, optr + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        GS_HIP(hipStreamSynchronize(s));
+    }
+    const int64_t nov = c->reg_nov;
     int64_t *dch;
     {
-        int64_t hch[4 * kRegMaxChunks] = {};
+        c->reg_hch.assign(4 * kRegMaxChunks, 0);
+        int64_t *hch = c->reg_hch.data();
         for (int t = 0; t < T; ++t) {
             hch[t] = ha[t];
             hch[kRegMaxChunks + t] = hlen[t];
             hch[2 * kRegMaxChunks + t] = keep[t];
             hch[3 * kRegMaxChunks + t] = lbase[t];
         }
-        dch = (int64_t *)c->buf("er_reg_chunks").ensure(sizeof(hch));
-        GS_HIP(hipMemcpy(dch, hch, sizeof(hch), hipMemcpyHostToDevice));
+        dch = (int64_t *)c->buf("er_reg_chunks").ensure(sizeof(int64_t) * 4 * kRegMaxChunks);
+        // stream-ordered; the host table lives in the context until the next solve
+        GS_HIP(hipMemcpyAsync(dch, hch, sizeof(int64_t) * 4 * kRegMaxChunks, hipMemcpyHostToDevice, s));
     }
     auto *ell = (uint4 *)c->buf("er_reg_ell").ensure(sizeof(uint4) * n);
     double *ellv = ufast ? nullptr : (double *)c->buf("er_reg_ellv").ensure(sizeof(double) * 8 * n);
     auto *ocol = (uint16_t *)c->buf("er_reg_ocol").ensure(sizeof(uint16_t) * (nov + 1));
     double *oval = ufast ? nullptr : (double *)c->buf("er_reg_oval").ensure(sizeof(double) * (nov + 1));
-    k_ell8_fill<<<grid_for(n, 256, 8192), 256, 0, s>>>(0, (int32_t)n, T, dch, pad, G, NT == 256 ? 2 : 1,
-                                                      ufast ? (int32_t)zs + 2 : -1, lp, li, lv, optr,
-                                                      ell, ellv, ocol, oval);
-    GS_HIP(hipGetLastError());
+    if (fresh) {
+        k_ell8_fill<<<grid_for(n, 256, 8192), 256, 0, s>>>(0, (int32_t)n, T, dch, pad, G, NT == 256 ? 2 : 1,
+                                                          ufast ? (int32_t)zs + 2 : -1, lp, li, lv, optr,
+                                                          ell, ellv, ocol, oval);
+        GS_HIP(hipGetLastError());
+        c->reg_ell_key = key;
+    }
     RegArgs A{};
-    // 512-thread form: q kept in registers from the SpMV pass to the r update, x in Xc
-    // (GSPARSE_REG_QR=0: q recomputed in the r update, x in registers)
-    A.qreg = 1;
+    // 512-thread form, whole columns: x in registers, q recomputed in the r update
+    // (GSPARSE_REG_QR=1: q kept in registers from the SpMV pass, x read-modify-written
+    // in Xc every iteration -- ~6x the fabric traffic for a wash in time).
+    // The split form always keeps q in registers (its x lives in Xc).
+    A.qreg = 0;
     if (const char *e = getenv("GSPARSE_REG_QR")) A.qreg = atoi(e) != 0;
     // Split plan: the last round of columns, when it leaves at least half the CUs idle,
     // runs as groups of P workgroups per column (k_cg_regwide<..., SPLIT>), each part a
@@ -194,7 +212,7 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     GS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
     int P = 0;
     int64_t W = ncols;  // columns solved whole (the first W), the rest split
-    if (NT == 512 && A.qreg && T >= 2 && ncols > 0) {
+    if (NT == 512 && T >= 2 && ncols > 0 && !c->reg_split_off) {
         const char *se = getenv("GSPARSE_REG_SPLIT");
         const int forced = se ? atoi(se) : -1;
         if (forced >= 2) {
@@ -321,7 +339,10 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     double *ellvs = ufast ? nullptr : (double *)c->buf("er_reg_split_ellv").ensure(sizeof(double) * 8 * n);
     auto *ocols = (uint16_t *)c->buf("er_reg_split_ocol").ensure(sizeof(uint16_t) * (nov + 1));
     double *ovals = ufast ? nullptr : (double *)c->buf("er_reg_split_oval").ensure(sizeof(double) * (nov + 1));
-    for (int h = 0; h < P; ++h) {
+    std::vector<int64_t> skey = {P, Gs};
+    skey.insert(skey.end(), pc0, pc0 + P + 1);
+    const bool sfresh = skey != c->reg_split_key;
+    for (int h = 0; h < P && sfresh; ++h) {
         const int32_t r0 = (int32_t)ha[pc0[h]];
         const int32_t r1 = (int32_t)(ha[pc0[h + 1] - 1] + hlen[pc0[h + 1] - 1]);
         const int32_t zsh = hpt[h * kRegPartTab + 4 * kRegMaxChunks + 1];
@@ -330,6 +351,7 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
             ufast ? zsh + 2 : -1, lp, li, lv, optr, ells, ellvs, ocols, ovals);
         GS_HIP(hipGetLastError());
     }
+    c->reg_split_key = skey;
     double *pgs = (double *)c->buf("er_reg_split_pg").ensure(sizeof(double) * (size_t)groups * 2 * ldn);
     double *xch = (double *)c->buf("er_reg_split_xch").ensure(sizeof(double) * (size_t)groups * 2 * kRegMaxChunks);
     auto *flg = (int32_t *)c->buf("er_reg_split_flags").ensure(sizeof(int32_t) * ((size_t)groups * P + 1));
@@ -349,7 +371,11 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     B.xch = xch;
     B.flags = flg;
     B.abortf = flg + (size_t)groups * P;
-    B.spinmax = 1 << 22;  // polls before a hand-off gives up (a few seconds)
+    // a hand-off waits at most 20 ms (a column-iteration of a split column takes
+    // ~30 us; a part that is not resident never arrives)
+    int wclk_khz = 100000;
+    GS_HIP(hipDeviceGetAttribute(&wclk_khz, hipDeviceAttributeWallClockRate, c->device));
+    B.spinmax = 20 * std::max(wclk_khz, 1);
     if (const char *e = getenv("GSPARSE_REG_SPLIT_SPIN")) B.spinmax = atoi(e);
     const unsigned grid = (unsigned)(groups * P);
     launch_whole();
@@ -361,8 +387,12 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     GS_HIP(hipStreamSynchronize(s));
     if (aborted) {
         // the parts of a column could not all be resident at once (another process or
-        // stream held CUs): solve the tail columns again, whole, one workgroup each
-        fprintf(stderr, "[gsparse] split CG hand-off timed out (%d parts); tail re-solved whole\n", P);
+        // stream held CUs): solve the tail columns again, whole, one workgroup each, and
+        // keep the split form off for this context from now on
+        c->reg_split_off = true;
+        prof_note(c, "cg_split_abort");
+        fprintf(stderr, "[gsparse] split CG hand-off timed out (%d parts); tail re-solved whole, "
+                        "split form off for this context\n", P);
         RegArgs Cw = A;
         Cw.col0 = col0 + W;
         Cw.ncols = tailn;

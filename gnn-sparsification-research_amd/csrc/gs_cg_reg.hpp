@@ -68,7 +68,8 @@ struct RegArgs {
     double *xch;          // [groups][2][kRegMaxChunks] chunk dots by hand-off parity
     int32_t *flags;       // [groups][P] hand-off sequence numbers (zeroed before the launch)
     int32_t *abortf;      // set when a hand-off poll gave up
-    int32_t spinmax;      // polls before it gives up
+    int32_t spinmax;      // wait budget of one hand-off poll, in ticks of the 100 MHz
+                          // constant clock (wall_clock64); 0: give up at once
 };
 static constexpr int kRegPartTab = 4 * kRegMaxChunks + 4;
 

@@ -295,8 +295,8 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
 
     // SPLIT hand-off: every wave drains its (sc1) stores, then one lane raises this
     // part's flag to the next sequence number and polls the group's other flags.  A
-    // poll that never matches (a part that cannot arrive) gives up after a few seconds
-    // and sets the abort word: from then on this workgroup's hand-offs are barriers
+    // poll that never matches (a part that cannot arrive) gives up after A.spinmax
+    // ticks of the constant clock (20 ms by default) and sets the abort word: from then on this workgroup's hand-offs are barriers
     // only, so the launch runs out (its results are discarded, the host reports the
     // abort) instead of hanging the GPU.  (No early return: a divergent exit from the
     // column loop breaks the uniform-register allocation of this kernel.)
@@ -310,11 +310,13 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         if (tid == 0 && !bad) {
             int verdict = 0;
             __hip_atomic_store(gflags + part, hseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the budget is wall time (a part that is not resident at all never arrives;
+            // one that is arrives within a column-iteration, tens of microseconds)
+            const uint64_t t_wait = wall_clock64();
             for (int q = 0; q < A.P && !verdict; ++q) {
                 if (q == part) continue;
-                for (int spin = 0; __hip_atomic_load(gflags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hseq;
-                     ++spin) {
-                    if (spin >= A.spinmax) {
+                while (__hip_atomic_load(gflags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hseq) {
+                    if (wall_clock64() - t_wait >= (uint64_t)A.spinmax) {
                         verdict = 1;
                         __hip_atomic_store(A.abortf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;

@@ -35,6 +35,16 @@ void prof_end(gs_ctx *c, hipEvent_t start, const char *name, double bytes) {
     if (c->pending.size() > 4096) prof_flush(c);
 }
 
+void prof_note(gs_ctx *c, const char *name) {
+    if (!c->profiling) return;
+    auto it = c->prof.find(name);
+    if (it == c->prof.end()) {
+        c->prof_order.push_back(name);
+        it = c->prof.emplace(name, ProfEntry{}).first;
+    }
+    it->second.launches += 1;
+}
+
 void prof_flush(gs_ctx *c) {
     if (c->pending.empty()) return;
     GS_HIP(hipStreamSynchronize(c->stream));

@@ -43,7 +43,8 @@ static Chunks make_chunks(int64_t n, int32_t threads) {
         ch.len[0] = n;
         return ch;
     }
-    if (threads > kMaxChunks) threads = kMaxChunks;
+    // OpenBLAS's own thread limit (MAX_THREADS=64 in NumPy's build): more threads
+    // cannot occur in the reference and are refused in gs_er_solve
     int64_t lo = 0, rem = n;
     int32_t cnt = 0;
     for (int32_t t = threads; t > 0 && rem > 0; --t) {
@@ -1613,6 +1614,7 @@ int gs_er_prepare(gs_ctx *c, int64_t k, double reg, int64_t *m_out) {
         int64_t n = g.n, nnz = g.nnz;
         er.n = n;
         er.k = k;
+        er.reg = reg;
         er.proj_next = 0;
         er.solved = false;
         // undirected edge ids (u<v in CSR order, metrics.py:236-242)
@@ -1724,6 +1726,9 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
         GS_CHECK(0 <= col0 && col0 < col1 && col1 <= er.k, GS_EINVAL, "bad column range");
         GS_HIP(hipSetDevice(c->device));
         const int64_t n = er.n, k = er.k;
+        GS_CHECK(blas_threads <= kMaxChunks || n <= 10000, GS_EUNSUPPORTED,
+                 "blas_threads=%d: the OpenBLAS ddot order is reproduced for at most %d threads "
+                 "(NumPy's OpenBLAS is built with MAX_THREADS=64)", blas_threads, kMaxChunks);
         ChunkArg ch = to_arg(make_chunks(n, blas_threads));
         // two columns per lane (16-B accesses) unless that leaves too few waves
         const int64_t ncols = col1 - col0;

@@ -176,6 +176,7 @@ static void reset_derived(gs_ctx *c) {
 
 static void finish_graph(gs_ctx *c) {
     Graph &g = c->g;
+    ++g.epoch;
     g.has_transpose = false;
     g.symmetric = 0;
     // Drop any ER state bound to the old graph.

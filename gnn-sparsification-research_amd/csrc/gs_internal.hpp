@@ -85,6 +85,17 @@ struct Graph {
     DevBuf tidx;      // int32 [nnz]
     DevBuf tpos;      // int64 [nnz] CSR position of each transposed entry
     bool has_transpose = false;
+    int64_t epoch = 0;  // bumped whenever a new graph is set (keys the per-graph caches)
+};
+
+// Row ranges of the sharded Jaccard (gs_jaccard_shares): cuts = [R | E | O], P + 1
+// values each -- cut rows, their first CSR entries, owner entries before them
+struct JacShares {
+    std::vector<int64_t> cuts;
+    int P() const { return (int)(cuts.size() / 3) - 1; }
+    int64_t R(int r) const { return cuts[r]; }
+    int64_t E(int r) const { return cuts[P() + 1 + r]; }
+    int64_t O(int r) const { return cuts[2 * (P() + 1) + r]; }
 };
 
 struct ErState {
@@ -92,6 +103,7 @@ struct ErState {
     int64_t ld = 0;         // row stride of the n x k arrays (k rounded up to 8)
     int64_t lnnz = 0;       // entries of L_reg
     int64_t proj_next = 0;  // next R row expected by project_rows
+    double reg = 0.0;       // L_reg = L + reg I of the last gs_er_prepare
     DevBuf edge_id;   // int64 [nnz] undirected edge id of CSR entry (u<v), -1 otherwise
     DevBuf bptr;      // int64 [n+1] incidence rows (B, metrics.py:260-269)
     DevBuf bcol;      // int64 [2m] edge id (ascending within row)
@@ -126,6 +138,16 @@ struct gs_ctx {
     gs::DevBuf scratch[6];
     gs::DevBuf outbuf, inbuf, inbuf2;
     std::map<std::string, gs::DevBuf> named;  // per-subsystem buffers (backbone, ...)
+    std::map<int, gs::JacShares> jac_shares;  // sharded Jaccard row ranges, by part count
+    int64_t jac_epoch = -1;                   // graph epoch jac_shares belong to
+    // register-resident CG (gs_cg_reg.hip): the ELL-8 copies are kept while their key
+    // (graph epoch, L_reg shift, chunk / LDS layout) is unchanged; the split form is
+    // switched off for the context after a hand-off gave up (its parts could not all
+    // be resident: another process or stream held CUs)
+    std::vector<int64_t> reg_ell_key, reg_split_key;
+    int64_t reg_nov = 0;
+    std::vector<int64_t> reg_hch;  // host copy of the chunk table (outlives its async copy)
+    bool reg_split_off = false;
     gs::DevBuf &buf(const char *name) { return named[name]; }
 };
 
@@ -134,6 +156,8 @@ namespace gs {
 // Record a profiled launch: call prof_begin before the launch and prof_end after.
 hipEvent_t prof_begin(gs_ctx *c);
 void prof_end(gs_ctx *c, hipEvent_t start, const char *name, double bytes);
+// count an event under `name` in the profile (launches += 1, no time)
+void prof_note(gs_ctx *c, const char *name);
 void prof_flush(gs_ctx *c);
 void sync_if_needed(gs_ctx *c);
 
@@ -187,7 +211,11 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
 
 // Whole-graph Jaccard of a symmetric graph (gs_jaccard.hip)
 // counts != 0: |N(u) ∩ N(v)| per entry instead of the Jaccard ratio
-void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts = 0);
+// cc != nullptr: the part's raw counts into its compact owner-entry array
+void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts = 0,
+                       uint32_t *cc = nullptr);
+const JacShares &jaccard_shares(gs_ctx *c, int P);
+void jaccard_from_counts(gs_ctx *c, int P, const uint32_t *cc, int64_t stride, double *out);
 
 // Dense grounded-Laplacian machinery (gs_exact_er.hip): component labels of the
 // resident graph (smallest node id per component, device), and W = L^{-1} of

@@ -47,6 +47,27 @@ __device__ __forceinline__ double jac_out(int counts, int64_t inter, int64_t du,
     return counts ? (double)inter : jac_value(inter, du, dv);
 }
 
+// Where a pair's result goes: both CSR entries of the full score vector (out,
+// rev = tpos), or -- the sharded form (gs_jaccard_part_counts) -- the raw count
+// into this part's compact owner-entry array cc[opre[e] - obase]
+struct JacSink {
+    double *out;
+    const int64_t *rev;
+    int counts;
+    uint32_t *cc;
+    const int64_t *opre;
+    int64_t obase;
+    __device__ __forceinline__ void put(int64_t e, int64_t cnt, int64_t du, int64_t dv) const {
+        if (cc) {
+            cc[opre[e] - obase] = (uint32_t)cnt;
+            return;
+        }
+        const double val = jac_out(counts, cnt, du, dv);
+        out[e] = val;
+        out[rev[e]] = val;
+    }
+};
+
 __host__ __device__ __forceinline__ int jac_class(int64_t d) {
     if (d <= kJacLight) return -1;
     if (d <= 1024) return 0;
@@ -63,16 +84,30 @@ __host__ __device__ __forceinline__ int64_t jac_task_probes(int k, int64_t du) {
     return t > kJacTaskMin ? t : kJacTaskMin;
 }
 
-// per row (one wave each): class, task count (work = sum of d_v over owned entries)
+// task count of a row of class k >= 0 with owned-entry probe work w (sum of d_v)
+__host__ __device__ __forceinline__ int64_t jac_row_tasks(int k, int64_t du, int64_t w) {
+    if (k < 0 || !w) return 0;
+    const int64_t t = jac_task_probes(k, du);
+    int64_t nt = (w + t - 1) / t;
+    const int64_t ne = (du + kJacMaxEnt - 1) / kJacMaxEnt;
+    if (nt < ne) nt = ne;
+    if (nt > du) nt = du;
+    return nt;
+}
+
+// per row (one wave each): class, task count (work = sum of d_v over owned entries);
+// tot[0..5] = per-class task totals ([kJacClasses]: rows with bitmap tasks),
+// tot[6..10] / tot[11..15] = tasks of rows below r0 / r1 (a part's task range)
 __global__ void __launch_bounds__(256) k_jac_plan(const int64_t *__restrict__ ip,
                                                   const int32_t *__restrict__ ix, int64_t n,
+                                                  int64_t r0, int64_t r1,
                                                   int8_t *__restrict__ cls,
                                                   int32_t *__restrict__ ntask,
                                                   unsigned long long *__restrict__ tot) {
     const int lane = threadIdx.x & 63;
     const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    unsigned long long mine[kJacClasses + 1] = {};  // lane 0: this wave's task totals
+    unsigned long long mine[3 * kJacClasses + 1] = {};  // lane 0: this wave's task totals
     for (int64_t u = w0; u < n; u += nw) {
         const int64_t a = ip[u], du = ip[u + 1] - a;
         const int k = jac_class(du);
@@ -86,32 +121,114 @@ __global__ void __launch_bounds__(256) k_jac_plan(const int64_t *__restrict__ ip
             for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o);
         }
         if (lane == 0) {
-            int64_t nt = 0;
-            if (k >= 0 && w) {
-                const int64_t t = jac_task_probes(k, du);
-                nt = (w + t - 1) / t;
-                const int64_t ne = (du + kJacMaxEnt - 1) / kJacMaxEnt;
-                if (nt < ne) nt = ne;
-                if (nt > du) nt = du;
-            }
+            const int64_t nt = jac_row_tasks(k, du, w);
             cls[u] = (int8_t)k;
             ntask[u] = (int32_t)nt;
-            if (nt) {  // per-class task totals; [kJacClasses] = rows with bitmap tasks
+            if (nt) {
+                const unsigned long long b0 = u < r0 ? 1ull : 0ull, b1 = u < r1 ? 1ull : 0ull;
 #pragma unroll
-                for (int q = 0; q < kJacClasses; ++q) mine[q] += q == k ? (unsigned long long)nt : 0ull;
+                for (int q = 0; q < kJacClasses; ++q) {
+                    const unsigned long long a = q == k ? (unsigned long long)nt : 0ull;
+                    mine[q] += a;
+                    mine[kJacClasses + 1 + q] += a * b0;
+                    mine[2 * kJacClasses + 1 + q] += a * b1;
+                }
                 mine[kJacClasses] += k == kJacBitmap ? 1ull : 0ull;
             }
         }
     }
-    __shared__ unsigned long long red[kJacClasses + 1];
-    if (threadIdx.x < kJacClasses + 1) red[threadIdx.x] = 0;
+    constexpr int NT = 3 * kJacClasses + 1;
+    __shared__ unsigned long long red[NT];
+    if (threadIdx.x < NT) red[threadIdx.x] = 0;
     __syncthreads();
     if (lane == 0)
 #pragma unroll
-        for (int q = 0; q <= kJacClasses; ++q)
+        for (int q = 0; q < NT; ++q)
             if (mine[q]) atomicAdd(&red[q], mine[q]);
     __syncthreads();
-    if (threadIdx.x < kJacClasses + 1 && red[threadIdx.x]) atomicAdd(&tot[threadIdx.x], red[threadIdx.x]);
+    if (threadIdx.x < NT && red[threadIdx.x]) atomicAdd(&tot[threadIdx.x], red[threadIdx.x]);
+}
+
+// Sharded form (gs_jaccard_shares): per-row intersection work of the owner entries
+// -- light rows d_u + d_v per owned entry (the merge), other rows d_v per owned entry
+// (the probes) plus d_u per task (the table build) -- for cutting the rows into
+// contiguous ranges of equal work
+__global__ void __launch_bounds__(256) k_jac_rowwork(const int64_t *__restrict__ ip,
+                                                     const int32_t *__restrict__ ix, int64_t n,
+                                                     int64_t *__restrict__ work) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t u = w0; u < n; u += nw) {
+        const int64_t a = ip[u], du = ip[u + 1] - a;
+        const int k = jac_class(du);
+        int64_t w = 0;
+        for (int64_t e = a + lane; e < a + du; e += 64) {
+            const int32_t v = ix[e];
+            const int64_t dv = ip[v + 1] - ip[v];
+            if (jac_owns(du, dv, (int32_t)u, v)) w += k < 0 ? du + dv : dv;
+        }
+        for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o);
+        if (lane == 0) work[u] = w + jac_row_tasks(k, du, w) * du;
+    }
+}
+
+// owner flag of every CSR entry (1: the entry (u, v) is its pair's owner entry)
+__global__ void k_jac_owner_flags(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                                  const int32_t *__restrict__ rows, int64_t nnz,
+                                  int64_t *__restrict__ flag) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t u = rows[e], v = ix[e];
+        flag[e] = jac_owns(ip[u + 1] - ip[u], ip[v + 1] - ip[v], u, v) ? 1 : 0;
+    }
+}
+
+// cut rows: R[r] = first row u with S[u] >= total * r / P (S: exclusive prefix of the
+// row work, S[n] = total), R[0] = 0, R[P] = n; then E[r] = ip[R[r]] and
+// O[r] = opre[E[r]].  One thread per cut.  out = [R | E | O], 3 (P + 1) values.
+__global__ void k_jac_cuts(const int64_t *__restrict__ S, const int64_t *__restrict__ ip,
+                           const int64_t *__restrict__ opre, int64_t n, int P,
+                           int64_t *__restrict__ out) {
+    const int r = threadIdx.x;
+    if (r > P) return;
+    const int64_t total = S[n];
+    int64_t R;
+    if (r == 0) R = 0;
+    else if (r == P) R = n;
+    else {
+        const int64_t t = total * r / P;
+        int64_t lo = 0, hi = n;  // first u in [0, n] with S[u] >= t
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (S[mid] >= t) hi = mid;
+            else lo = mid + 1;
+        }
+        R = lo;
+    }
+    out[r] = R;
+    out[P + 1 + r] = ip[R];
+    out[2 * (P + 1) + r] = opre[ip[R]];
+}
+
+// sharded form: every part's counts -> both CSR entries of each pair
+__global__ void k_jac_from_counts(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                                  const int32_t *__restrict__ rows, const int64_t *__restrict__ rev,
+                                  const int64_t *__restrict__ opre, const int64_t *__restrict__ cuts,
+                                  int P, const uint32_t *__restrict__ cc, int64_t stride,
+                                  int64_t nnz, double *__restrict__ out) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t u = rows[e], v = ix[e];
+        const int64_t du = ip[u + 1] - ip[u], dv = ip[v + 1] - ip[v];
+        if (!jac_owns(du, dv, u, v)) continue;
+        int r = 0;  // part whose row range holds u: cuts[0..P] = R
+        while (r + 1 < P && u >= cuts[r + 1]) ++r;
+        const int64_t cnt = cc[r * stride + (opre[e] - cuts[2 * (P + 1) + r])];
+        const double val = jac_value(cnt, du, dv);
+        out[e] = val;
+        out[rev[e]] = val;
+    }
 }
 
 __global__ void k_jac_mask(const int8_t *__restrict__ cls, const int32_t *__restrict__ ntask,
@@ -149,9 +266,7 @@ __global__ void k_jac_emit(const int8_t *__restrict__ cls, const int32_t *__rest
 __global__ void __launch_bounds__(256) k_jac_light(const int64_t *__restrict__ ip,
                                                    const int32_t *__restrict__ ix,
                                                    const int32_t *__restrict__ rows,
-                                                   const int64_t *__restrict__ rev, int64_t e0,
-                                                   int64_t e1, double *__restrict__ out,
-                                                   int counts) {
+                                                   int64_t e0, int64_t e1, JacSink sk) {
     for (int64_t e = e0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < e1;
          e += (int64_t)gridDim.x * blockDim.x) {
         const int32_t u = rows[e];
@@ -167,9 +282,7 @@ __global__ void __launch_bounds__(256) k_jac_light(const int64_t *__restrict__ i
             i += (x <= y);
             j += (y <= x);
         }
-        const double val = jac_out(counts, cnt, du, dv);
-        out[e] = val;
-        out[rev[e]] = val;
+        sk.put(e, cnt, du, dv);
     }
 }
 
@@ -236,11 +349,9 @@ struct JacBitProbe {
 // Probe phase shared by the LDS-table and bitmap kernels (after jac_stage and
 // a barrier).  The d_u of the owner and each entry's d_v give the union.
 template <class Probe>
-__device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
-                                                 const int64_t *__restrict__ rev, int64_t du,
+__device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix, int64_t du,
                                                  int64_t lo, const JacStage &st,
-                                                 double *__restrict__ out, const Probe &pr,
-                                                 int counts) {
+                                                 const JacSink &sk, const Probe &pr) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     for (int k = wave; k < st.nbig; k += nw) {
         const int64_t b = st.b[k], dv = st.dv[k];
@@ -261,12 +372,7 @@ __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
                 cnt += __popcll(__ballot(hit));
             }
         }
-        if (lane == 0) {
-            const int64_t e = lo + st.off[k];
-            const double val = jac_out(counts, cnt, du, dv);
-            out[e] = val;
-            out[rev[e]] = val;
-        }
+        if (lane == 0) sk.put(lo + st.off[k], cnt, du, dv);
     }
     const int grp = lane >> 4, gl = lane & 15;
     const uint64_t gmask = 0xFFFFull << (16 * grp);
@@ -279,12 +385,7 @@ __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
         const typename Probe::S ps = pr.first(x >= 0 ? x : 0);
         const bool hit = x >= 0 && pr.done(x, ps);
         const int64_t cnt = __popcll(__ballot(hit) & gmask);
-        if (ok && gl == 0) {
-            const int64_t e = lo + st.off[k];
-            const double val = jac_out(counts, cnt, du, dv);
-            out[e] = val;
-            out[rev[e]] = val;
-        }
+        if (ok && gl == 0) sk.put(lo + st.off[k], cnt, du, dv);
     }
 }
 
@@ -303,11 +404,10 @@ __device__ __forceinline__ void jac_task_range(const int64_t *__restrict__ ip,
 template <int C>
 __global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ ip,
                                                    const int32_t *__restrict__ ix,
-                                                   const int64_t *__restrict__ rev,
                                                    const int32_t *__restrict__ ntask,
                                                    const int32_t *__restrict__ trow,
                                                    const int32_t *__restrict__ ti, int64_t t0,
-                                                   double *__restrict__ out, int counts) {
+                                                   JacSink sk) {
     // 4-slot buckets (one 16-B LDS read per probe step); a bucket fills from
     // slot 0 up, so a bucket with a free slot 3 ends an unsuccessful search
     __shared__ int4 tab[C / 4];
@@ -337,7 +437,7 @@ __global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ i
         }
     }
     __syncthreads();
-    jac_probe_staged(ix, rev, du, lo, st, out, JacHashProbe{tab, shift, mask}, counts);
+    jac_probe_staged(ix, du, lo, st, sk, JacHashProbe{tab, shift, mask});
 }
 
 __global__ void k_jac_bitmap_build(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
@@ -354,14 +454,12 @@ __global__ void k_jac_bitmap_build(const int64_t *__restrict__ ip, const int32_t
 
 __global__ void __launch_bounds__(1024) k_jac_bitmap(const int64_t *__restrict__ ip,
                                                      const int32_t *__restrict__ ix,
-                                                     const int64_t *__restrict__ rev,
                                                      const int32_t *__restrict__ ntask,
                                                      const int32_t *__restrict__ trow,
                                                      const int32_t *__restrict__ ti,
                                                      const int32_t *__restrict__ tslot,
                                                      int64_t t0, int32_t g0, int64_t words,
-                                                     const uint32_t *__restrict__ bm,
-                                                     double *__restrict__ out, int counts) {
+                                                     const uint32_t *__restrict__ bm, JacSink sk) {
     const int64_t t = t0 + blockIdx.x;
     const int32_t u = trow[t];
     int64_t a, du, lo, hi;
@@ -372,7 +470,7 @@ __global__ void __launch_bounds__(1024) k_jac_bitmap(const int64_t *__restrict__
     __syncthreads();
     jac_stage(ip, ix, u, du, lo, hi, st);
     __syncthreads();
-    jac_probe_staged(ix, rev, du, lo, st, out, JacBitProbe{m}, counts);
+    jac_probe_staged(ix, du, lo, st, sk, JacBitProbe{m});
 }
 
 // B_J for a symmetric graph: 8 * sum_u d_u^2 + 12 * nnz
@@ -388,20 +486,70 @@ __global__ void k_jac_bytes(const int64_t *__restrict__ ip, int64_t n,
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(acc, s);
 }
 
+// Row ranges of the sharded form (cached per graph and part count): R[0..P] cut
+// rows, E[r] = ip[R[r]], O[r] = owner entries before E[r]; opre (device) = the
+// exclusive prefix of the owner flags over the CSR entries
+const JacShares &jaccard_shares(gs_ctx *c, int P) {
+    Graph &g = c->g;
+    if (c->jac_epoch != g.epoch) {
+        c->jac_shares.clear();
+        c->jac_epoch = g.epoch;
+    }
+    auto it = c->jac_shares.find(P);
+    if (it != c->jac_shares.end()) return it->second;
+    const int64_t n = g.n, nnz = g.nnz;
+    hipStream_t st = c->stream;
+    const int64_t *ip = g.indptr.as<int64_t>();
+    const int32_t *ix = g.indices.as<int32_t>();
+    auto *opre = (int64_t *)c->buf("jac_opre").ensure(sizeof(int64_t) * (nnz + 1));
+    if (c->jac_shares.empty()) {  // the owner prefix is the same for every P
+        auto *fl = (int64_t *)c->buf("jac_oflag").ensure(sizeof(int64_t) * (nnz + 1));
+        GS_HIP(hipMemsetAsync(fl + nnz, 0, sizeof(int64_t), st));
+        if (nnz)
+            k_jac_owner_flags<<<grid_for(nnz, 256, 65536), 256, 0, st>>>(ip, ix, g.rows.as<int32_t>(),
+                                                                         nnz, fl);
+        exclusive_scan_i64(c, fl, opre, nnz + 1);
+        c->buf("jac_oflag").release();
+    }
+    auto *work = (int64_t *)c->buf("jac_work").ensure(sizeof(int64_t) * (n + 1));
+    auto *S = (int64_t *)c->buf("jac_wpre").ensure(sizeof(int64_t) * (n + 1));
+    GS_HIP(hipMemsetAsync(work + n, 0, sizeof(int64_t), st));
+    if (n) k_jac_rowwork<<<grid_for(n, 4, 4096), 256, 0, st>>>(ip, ix, n, work);
+    exclusive_scan_i64(c, work, S, n + 1);
+    auto *dcut = (int64_t *)c->buf("jac_cutbuf").ensure(sizeof(int64_t) * 3 * (P + 1));
+    k_jac_cuts<<<1, 128, 0, st>>>(S, ip, opre, n, P, dcut);
+    GS_HIP(hipGetLastError());
+    JacShares sh;
+    sh.cuts.resize(3 * (P + 1));
+    GS_HIP(hipMemcpyAsync(sh.cuts.data(), dcut, sizeof(int64_t) * 3 * (P + 1), hipMemcpyDeviceToHost, st));
+    GS_HIP(hipStreamSynchronize(st));
+    c->buf("jac_work").release();
+    c->buf("jac_wpre").release();
+    return c->jac_shares.emplace(P, std::move(sh)).first->second;
+}
+
 // Whole-graph Jaccard of a symmetric graph into device out[nnz], or part
-// `part` of `nparts` of it: that part's share of the light entries and of
-// every class's task list (both CSR entries of each pair written), every
-// other entry 0.0 -- the nparts outputs sum to the whole.
-void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts) {
+// `part` of `nparts` of it: the owner entries of that part's rows (jaccard_shares),
+// both CSR entries of each pair written into out (every other entry 0.0, so the
+// nparts outputs sum to the whole) -- or, with cc, the raw counts into the part's
+// compact owner-entry array (gs_jaccard_part_counts).
+void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts, uint32_t *cc) {
     Graph &g = c->g;
     const int64_t n = g.n, nnz = g.nnz;
     if (!nnz) return;
     hipStream_t st = c->stream;
-    auto share = [&](int64_t total, int p) { return total * p / nparts; };
-    if (nparts > 1) GS_HIP(hipMemsetAsync(out, 0, sizeof(double) * nnz, st));
     const int64_t *ip = g.indptr.as<int64_t>();
     const int32_t *ix = g.indices.as<int32_t>();
     const int64_t *rev = g.tpos.as<int64_t>();
+    int64_t r0 = 0, r1 = n, e0 = 0, e1 = nnz, obase = 0;
+    if (nparts > 1) {
+        const JacShares &sh = jaccard_shares(c, nparts);
+        r0 = sh.R(part), r1 = sh.R(part + 1);
+        e0 = sh.E(part), e1 = sh.E(part + 1);
+        obase = sh.O(part);
+    }
+    if (nparts > 1 && !cc) GS_HIP(hipMemsetAsync(out, 0, sizeof(double) * nnz, st));
+    JacSink sk{out, rev, counts, cc, cc ? c->buf("jac_opre").as<int64_t>() : nullptr, obase};
     double algo = 0.0;
     if (c->profiling) {
         auto *acc = (unsigned long long *)c->buf("jac_bytes").ensure(8);
@@ -410,7 +558,7 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts)
         unsigned long long s = 0;
         GS_HIP(hipMemcpyAsync(&s, acc, 8, hipMemcpyDeviceToHost, st));
         GS_HIP(hipStreamSynchronize(st));
-        algo = 8.0 * (double)s + 12.0 * (double)nnz;
+        algo = (8.0 * (double)s + 12.0 * (double)nnz) * (nnz ? (double)(e1 - e0) / (double)nnz : 0.0);
     }
     hipEvent_t t0 = prof_begin(c);
     auto *cls = (int8_t *)c->buf("jac_cls").ensure(n);
@@ -419,17 +567,15 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts)
     auto *off = (int64_t *)c->buf("jac_off").ensure(sizeof(int64_t) * (n + 1));
     auto *gfl = (int64_t *)c->buf("jac_gflag").ensure(sizeof(int64_t) * (n + 1));
     auto *goff = (int64_t *)c->buf("jac_goff").ensure(sizeof(int64_t) * (n + 1));
-    auto *dtot = (unsigned long long *)c->buf("jac_tot").ensure(8 * (kJacClasses + 1));
-    GS_HIP(hipMemsetAsync(dtot, 0, 8 * (kJacClasses + 1), st));
-    k_jac_plan<<<grid_for(n, 4, 4096), 256, 0, st>>>(ip, ix, n, cls, ntask, dtot);
-    {
-        const int64_t e0 = share(nnz, part), e1 = share(nnz, part + 1);
-        if (e1 > e0)
-            k_jac_light<<<grid_for(e1 - e0, 256, 65536), 256, 0, st>>>(
-                ip, ix, g.rows.as<int32_t>(), rev, e0, e1, out, counts);
-    }
+    constexpr int kTot = 3 * kJacClasses + 1;
+    auto *dtot = (unsigned long long *)c->buf("jac_tot").ensure(8 * kTot);
+    GS_HIP(hipMemsetAsync(dtot, 0, 8 * kTot, st));
+    k_jac_plan<<<grid_for(n, 4, 4096), 256, 0, st>>>(ip, ix, n, r0, r1, cls, ntask, dtot);
+    if (e1 > e0)
+        k_jac_light<<<grid_for(e1 - e0, 256, 65536), 256, 0, st>>>(ip, ix, g.rows.as<int32_t>(), e0,
+                                                                   e1, sk);
     GS_HIP(hipGetLastError());
-    unsigned long long htot[kJacClasses + 1];
+    unsigned long long htot[kTot];
     GS_HIP(hipMemcpyAsync(htot, dtot, sizeof(htot), hipMemcpyDeviceToHost, st));
     GS_HIP(hipStreamSynchronize(st));  // the only sync unless bitmap rows exist
     int64_t tmax = 1;
@@ -437,7 +583,6 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts)
     // the hash classes run concurrently on side streams (a class of big LDS tables
     // fills one or two workgroups per CU; the others use the rest): each gets its own
     // task lists; the bitmap class stays on the context stream
-    (void)tmax;
     bool conc = true;
     if (const char *e = getenv("GSPARSE_JAC_CONCURRENT")) conc = atoi(e) != 0;
     if (conc) {
@@ -472,7 +617,8 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts)
                                                             n, k, trow, ti, tslot, grow);
         GS_HIP(hipGetLastError());
         GS_CHECK(ntot <= INT32_MAX, GS_EUNSUPPORTED, "too many Jaccard tasks (%lld)", (long long)ntot);
-        const int64_t tlo = share(ntot, part), thi = share(ntot, part + 1);
+        // this part's rows' tasks (tasks are emitted in row order)
+        const int64_t tlo = (int64_t)htot[kJacClasses + 1 + k], thi = (int64_t)htot[2 * kJacClasses + 1 + k];
         const unsigned nb = (unsigned)(thi - tlo);
         if (k < kJacBitmap && !nb) continue;
         // hash classes: on side stream k once the task lists are emitted
@@ -484,13 +630,13 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts)
             launched |= 1 << k;
         }
         if (k == 0) {
-            k_jac_hash<2048><<<nb, 256, 0, hs>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
+            k_jac_hash<2048><<<nb, 256, 0, hs>>>(ip, ix, ntask, trow, ti, tlo, sk);
         } else if (k == 1) {
-            k_jac_hash<8192><<<nb, 512, 0, hs>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
+            k_jac_hash<8192><<<nb, 512, 0, hs>>>(ip, ix, ntask, trow, ti, tlo, sk);
         } else if (k == 2) {
-            k_jac_hash<16384><<<nb, 1024, 0, hs>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
+            k_jac_hash<16384><<<nb, 1024, 0, hs>>>(ip, ix, ntask, trow, ti, tlo, sk);
         } else if (k == 3) {
-            k_jac_hash<32768><<<nb, 1024, 0, hs>>>(ip, ix, rev, ntask, trow, ti, tlo, out, counts);
+            k_jac_hash<32768><<<nb, 1024, 0, hs>>>(ip, ix, ntask, trow, ti, tlo, sk);
         } else {
             // bitmaps in batches of rows (<= 1 GiB of bits at a time)
             const int64_t words = (n + 31) / 32;
@@ -519,7 +665,7 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts)
                     ip, ix, grow, (int32_t)g0, words, bm);
                 if (tb[1] > tb[0])
                     k_jac_bitmap<<<(unsigned)(tb[1] - tb[0]), 1024, 0, st>>>(
-                        ip, ix, rev, ntask, trow, ti, tslot, tb[0], (int32_t)g0, words, bm, out, counts);
+                        ip, ix, ntask, trow, ti, tslot, tb[0], (int32_t)g0, words, bm, sk);
                 GS_HIP(hipGetLastError());
             }
         }
@@ -532,6 +678,30 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts)
             GS_HIP(hipStreamWaitEvent(st, c->aux_ev[k], 0));
         }
     prof_end(c, t0, counts ? "common_neighbors" : "jaccard", algo);
+}
+
+// gs_jaccard_from_counts: every part's counts -> the Jaccard score of every entry
+void jaccard_from_counts(gs_ctx *c, int P, const uint32_t *cc, int64_t stride, double *out) {
+    Graph &g = c->g;
+    const int64_t nnz = g.nnz;
+    if (!nnz) return;
+    const JacShares &sh = jaccard_shares(c, P);
+    for (int r = 0; r < P; ++r)
+        GS_CHECK(sh.O(r + 1) - sh.O(r) <= stride, GS_EINDEX,
+                 "part %d holds %lld owner pairs, more than the stride %lld", r,
+                 (long long)(sh.O(r + 1) - sh.O(r)), (long long)stride);
+    auto *dcut = (int64_t *)c->buf("jac_cutdev").ensure(sizeof(int64_t) * sh.cuts.size());
+    GS_HIP(hipMemcpyAsync(dcut, sh.cuts.data(), sizeof(int64_t) * sh.cuts.size(),
+                          hipMemcpyHostToDevice, c->stream));
+    hipEvent_t t0 = prof_begin(c);
+    k_jac_from_counts<<<grid_for(nnz, 256, 65536), 256, 0, c->stream>>>(
+        g.indptr.as<int64_t>(), g.indices.as<int32_t>(), g.rows.as<int32_t>(), g.tpos.as<int64_t>(),
+        c->buf("jac_opre").as<int64_t>(), dcut, P, cc, stride, nnz, out);
+    GS_HIP(hipGetLastError());
+    // reads rows, ix, opre, the endpoints' indptr and the counts; writes both entries
+    prof_end(c, t0, "jaccard_scatter", (double)nnz * (4.0 + 4.0 + 8.0 + 32.0) + 8.0 * (double)nnz +
+                                           2.0 * (double)sh.O(P));
+    // the host copy of cuts must outlive the async H2D copy: it lives in the cache
 }
 
 }  // namespace gs

@@ -283,6 +283,54 @@ int gs_jaccard_part(gs_ctx *c, int part, int nparts, double *out, int loc) {
     });
 }
 
+static void check_sharded_jaccard(gs_ctx *c, int nparts) {
+    GS_CHECK(c, GS_EINVAL, "null context");
+    GS_CHECK(nparts >= 1 && nparts <= 4096, GS_EINVAL, "bad part count %d", nparts);
+    GS_CHECK(c->g.has_transpose, GS_ESTATE, "no graph set");
+    GS_CHECK(c->g.symmetric, GS_EUNSUPPORTED,
+             "owner-pair shares need a symmetric graph (use edge ranges on a directed one)");
+}
+
+int gs_jaccard_shares(gs_ctx *c, int nparts, int64_t *row_cut, int64_t *owner_off) {
+    return guard([&] {
+        check_sharded_jaccard(c, nparts);
+        GS_HIP(hipSetDevice(c->device));
+        const JacShares &sh = jaccard_shares(c, nparts);
+        for (int r = 0; r <= nparts; ++r) {
+            if (row_cut) row_cut[r] = sh.R(r);
+            if (owner_off) owner_off[r] = sh.O(r);
+        }
+    });
+}
+
+int gs_jaccard_part_counts(gs_ctx *c, int part, int nparts, uint32_t *counts, int loc) {
+    return guard([&] {
+        check_sharded_jaccard(c, nparts);
+        GS_CHECK(0 <= part && part < nparts, GS_EINVAL, "bad part %d of %d", part, nparts);
+        GS_HIP(hipSetDevice(c->device));
+        const JacShares &sh = jaccard_shares(c, nparts);
+        const int64_t cnt = sh.O(part + 1) - sh.O(part);
+        auto *d = (uint32_t *)out_device(c, c->outbuf, counts, sizeof(uint32_t) * cnt, loc);
+        if (cnt) jaccard_symmetric(c, nullptr, part, nparts, 0, d);
+        finish_out(c, counts, d, sizeof(uint32_t) * cnt, loc);
+    });
+}
+
+int gs_jaccard_from_counts(gs_ctx *c, int nparts, const uint32_t *counts, int64_t stride,
+                           int c_loc, double *out, int loc) {
+    return guard([&] {
+        check_sharded_jaccard(c, nparts);
+        GS_CHECK(stride >= 0, GS_EINVAL, "negative stride");
+        GS_HIP(hipSetDevice(c->device));
+        const int64_t nnz = c->g.nnz;
+        const uint32_t *dc = (const uint32_t *)to_device(c, c->inbuf, counts,
+                                                         sizeof(uint32_t) * stride * nparts, c_loc);
+        double *dout = (double *)out_device(c, c->outbuf, out, sizeof(double) * nnz, loc);
+        jaccard_from_counts(c, nparts, dc, stride, dout);
+        finish_out(c, out, dout, sizeof(double) * nnz, loc);
+    });
+}
+
 int gs_adamic_adar(gs_ctx *c, const double *cw, int c_loc, int64_t e0, int64_t e1, double *out,
                    int loc) {
     return guard([&] {

@@ -48,6 +48,9 @@ SIGNATURES = {
     "gs_graph_copy_csr": (_int, [_vp, _vp, _vp, _vp, _int]),
     "gs_jaccard": (_int, [_vp, _i64, _i64, _vp, _int]),
     "gs_jaccard_part": (_int, [_vp, _int, _int, _vp, _int]),
+    "gs_jaccard_shares": (_int, [_vp, _int, _vp, _vp]),
+    "gs_jaccard_part_counts": (_int, [_vp, _int, _int, _vp, _int]),
+    "gs_jaccard_from_counts": (_int, [_vp, _int, _vp, _i64, _int, _vp, _int]),
     "gs_adamic_adar": (_int, [_vp, _vp, _int, _i64, _i64, _vp, _int]),
     "gs_degree": (_int, [_vp, _i64, _i64, _vp, _int]),
     "gs_feature_cosine_f32": (_int, [_vp, _vp, _i64, _int, _i64, _i64, _vp, _int]),
@@ -148,10 +151,35 @@ def device_count() -> int:
     return n.value
 
 
+def _torch_current_device() -> int | None:
+    """torch's current CUDA device when torch has initialised CUDA in this
+    process (a caller's ``torch.cuda.set_device(k)`` -- roman_empire_gpu.py:209
+    before ``GraphSparsifier(full_graph, device='cpu')`` at :213), else None.
+    Never initialises CUDA itself."""
+    import sys
+
+    torch = sys.modules.get("torch")
+    if torch is None:
+        return None
+    try:
+        if not torch.cuda.is_initialized():
+            return None
+        return int(torch.cuda.current_device())
+    except Exception:
+        return None
+
+
 def default_device() -> int:
+    """Device of a context created without an explicit ordinal:
+    $GSPARSE_DEVICE, else torch's current device once torch has initialised
+    CUDA (the caller's set_device), else $LOCAL_RANK (modulo the visible GPUs),
+    else 0."""
     env = os.environ.get("GSPARSE_DEVICE")
     if env is not None:
         return int(env)
+    cur = _torch_current_device()
+    if cur is not None:
+        return cur
     lr = os.environ.get("LOCAL_RANK")
     if lr is not None:
         # one process per GPU (roman_empire_gpu.py:347); more ranks than visible

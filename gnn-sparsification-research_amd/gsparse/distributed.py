@@ -1,12 +1,16 @@
 """Multi-GPU sharding of the scorers (one process per GPU, torch.distributed).
 
 SURVEY §8(e):
-  * Jaccard on a symmetric graph: each rank takes its share of the owner-side
-    pair tasks (gs_jaccard_part: both CSR entries of a pair, zeros elsewhere)
-    and one all-reduce(sum) assembles the whole vector -- exact, since every
-    entry has exactly one non-zero contributor.
+  * Jaccard on a symmetric graph: each undirected pair is intersected once, at
+    its owner endpoint; rank r takes the owner pairs of a contiguous row range
+    cut at equal shares of the intersection work (gs_jaccard_shares, the same
+    on every rank) and produces their integer counts (gs_jaccard_part_counts,
+    4 B per pair).  One all-gather of the counts, then every rank writes the
+    score of both CSR entries of every pair (gs_jaccard_from_counts: the
+    reference's single fp64 division) -- 2 B per directed edge on the wire
+    instead of the 8 B per edge of a score all-gather.
   * metric backbone: the per-source searches by source row (u % world), one
-    all-reduce(sum) of the keep bytes.
+    all-reduce(sum) of the uint8 keep bytes (each column has one contributor).
   * AA / degree / FeatCos (and Jaccard on explicit ranges): contiguous CSR
     edge ranges (equal counts, or equal per-edge work d_u + d_v for skewed
     graphs), then an all-gather of the fp64 scores so every rank can run the
@@ -15,7 +19,10 @@ SURVEY §8(e):
     nodes of NumPy's pairwise-sum tree over k (gs_er_split), so each rank's
     per-edge partial sum is exactly a subtree of the reference's
     ``np.sum(diff**2, axis=1)``; partials are all-gathered and added in tree
-    order -- scores are bit-identical for any power-of-two rank count.
+    order.  A power-of-two rank count takes one tree node per rank; any other
+    count takes contiguous runs of the nodes one level deeper than needed (down
+    to the tree's leaves) and sends the partial sums of the maximal subtrees of
+    its run, combined in tree order on every rank -- bit-identical for any N.
 The RCCL backend ("nccl") moves device tensors over xGMI; "gloo" (CPU
 tensors) runs the same code for tests and rehearsals.
 """
@@ -105,17 +112,46 @@ class Comm:
         dist.all_gather(out, local.to(self.device), group=self.group)
         return out
 
+    def all_gather_flat(self, local: torch.Tensor) -> torch.Tensor:
+        """Equal-size shards concatenated in rank order (one RCCL all-gather
+        into a flat buffer; gloo: list all-gather + cat)."""
+        local = local.to(self.device).contiguous()
+        if self.backend == "nccl":
+            out = torch.empty(self.world * local.numel(), dtype=local.dtype, device=self.device)
+            dist.all_gather_into_tensor(out, local, group=self.group)
+            return out
+        return torch.cat(self.all_gather_same(local))
+
+
+def sharded_jaccard(engine, comm: Comm, out=None):
+    """Jaccard of a symmetric graph over ranks: this rank's owner-pair counts,
+    one all-gather of the uint32 counts (padded to the largest share), scores of
+    every CSR entry on every rank -- bit-identical to engine.jaccard()."""
+    _, oo = engine.jaccard_shares(comm.world)
+    sizes = np.diff(oo)
+    stride = max(1, int(sizes.max()) if len(sizes) else 1)
+    if comm.device.type == "cuda":
+        buf = torch.zeros(stride, dtype=torch.int32, device=comm.device)
+        engine.jaccard_part_counts(comm.rank, comm.world, out=buf)
+    else:
+        buf = torch.zeros(stride, dtype=torch.int32)
+        part = np.asarray(engine.jaccard_part_counts(comm.rank, comm.world), dtype=np.uint32)
+        buf[: part.shape[0]] = torch.from_numpy(part.view(np.int32))
+    allc = comm.all_gather_flat(buf)
+    if comm.device.type == "cuda":
+        if out is None:
+            out = torch.empty(engine.nnz, dtype=torch.float64, device=comm.device)
+        return engine.jaccard_from_counts(comm.world, allc, stride, out=out)
+    return torch.from_numpy(np.asarray(
+        engine.jaccard_from_counts(comm.world, allc.numpy().view(np.uint32), stride)))
+
 
 def sharded_edge_scores(engine, comm: Comm, metric: str, bounds: list[int] | None = None,
                         **kw):
     """One scorer over this rank's CSR edge range, all-gathered to every rank."""
     nnz = engine.nnz
-    if metric == "jaccard" and bounds is None and hasattr(engine, "jaccard_part"):
-        out = None
-        if comm.device.type == "cuda":
-            out = torch.empty(nnz, dtype=torch.float64, device=comm.device)
-        part = engine.jaccard_part(comm.rank, comm.world, out=out)
-        return comm.all_reduce_sum(comm.tensor(part))
+    if metric == "jaccard" and bounds is None and getattr(engine, "symmetric", False):
+        return sharded_jaccard(engine, comm, out=kw.get("out"))
     b = bounds or edge_ranges(nnz, comm.world)
     e0, e1 = b[comm.rank], b[comm.rank + 1]
     fn = {"jaccard": engine.jaccard, "adamic_adar": engine.adamic_adar,
@@ -145,15 +181,60 @@ def sharded_backbone(comm: Comm, edge_index: np.ndarray, num_nodes: int,
         from .metric_backbone import backbone_mask as mask_fn
     part = mask_fn(edge_index, num_nodes, edge_weights, epsilon, part=comm.rank,
                    nparts=comm.world)
-    t = comm.tensor(np.ascontiguousarray(part, dtype=np.uint8).astype(np.int32))
+    t = comm.tensor(np.ascontiguousarray(part, dtype=np.uint8))
     return comm.all_reduce_sum(t).cpu().numpy().astype(bool)
+
+
+def er_rank_blocks(k: int, world: int, max_depth: int = 5):
+    """Column blocks of the pairwise tree of k for `world` ranks.
+
+    Returns (depth, bounds, runs): the 2**depth nodes of the tree at `depth`
+    (bounds, gs_er_split) and each rank's contiguous run [a, b) of them.  A
+    power-of-two world takes one node per rank at depth log2(world); any other
+    world the deepest level (<= max_depth, every node above it still split)
+    with runs cut at the node boundaries nearest the equal column shares -- so
+    every rank's columns are whole tree nodes whatever N is."""
+    from .engine import er_split
+
+    need = max(0, (world - 1).bit_length())
+    top = need if world & (world - 1) == 0 else max(need, max_depth)
+    # shallower levels when k is too small to split that far (some ranks idle)
+    depths = list(range(top, -1, -1))
+    for d in depths:
+        try:
+            bounds = er_split(k, 1 << d)
+        except ValueError:
+            continue
+        # run boundaries at the node boundary nearest each rank's equal column share
+        bnd = np.asarray(bounds)
+        cut = [0] + [int(np.argmin(np.abs(bnd - k * r / world))) for r in range(1, world)] \
+            + [len(bounds) - 1]
+        for r in range(1, world + 1):
+            cut[r] = max(cut[r], cut[r - 1])
+        runs = [(cut[r], cut[r + 1]) for r in range(world)]
+        return d, bounds, runs
+    return 0, [0, k], [(0, 1)] + [(1, 1)] * (world - 1)
+
+
+def dyadic_cover(a: int, b: int):
+    """Maximal dyadic blocks (level, index) covering frontier nodes [a, b):
+    level L block i spans nodes [i * 2**L, (i + 1) * 2**L) -- subtrees of the
+    pairwise tree whose partial sums a rank can fold locally."""
+    out = []
+    while a < b:
+        lev = 0
+        while a % (2 << lev) == 0 and a + (2 << lev) <= b:
+            lev += 1
+        out.append((lev, a >> lev))
+        a += 1 << lev
+    return out
 
 
 def sharded_approx_er(engine, comm: Comm, epsilon: float = 0.3, seed: int = 42,
                       max_cg_iters: int = 500, cg_tol: float = 1e-6, blas_threads: int = 1,
                       rng_mode: str = "device"):
     """ApproxER with the JL columns split over ranks along the pairwise tree."""
-    from .engine import er_split, jl_dim
+    from .engine import jl_dim
 
     n = engine.n
     k = jl_dim(n, epsilon)
@@ -161,26 +242,36 @@ def sharded_approx_er(engine, comm: Comm, epsilon: float = 0.3, seed: int = 42,
     m = engine.er_prepare(k)
     if m == 0:
         return comm.tensor(np.zeros(engine.nnz))
-    parts = pow2_floor(comm.world)
-    bounds = [0, k]
-    while parts > 1:  # every block must be a non-leaf node of the pairwise tree
-        try:
-            bounds = er_split(k, parts)
-            break
-        except ValueError:
-            parts //= 2
+    depth, bounds, runs = er_rank_blocks(k, comm.world)
     if rng_mode == "device":
         engine.er_project_device(rng, k)
     else:
         engine.er_project_host(rng, k)
-    if comm.rank < parts:
-        c0, c1 = bounds[comm.rank], bounds[comm.rank + 1]
-        engine.er_solve(c0, c1, max_cg_iters, cg_tol, blas_threads)
-        out = None
-        if comm.device.type == "cuda":
-            out = torch.empty(engine.nnz, dtype=torch.float64, device=comm.device)
-        local = comm.tensor(engine.er_scores(c0, c1, finalize=False, out=out))
-    else:
-        local = comm.tensor(np.zeros(engine.nnz))
-    gathered = comm.all_gather_same(local)
-    return finalize_er(tree_sum(gathered[:parts]))
+    covers = [dyadic_cover(a, b) for a, b in runs]
+    slots = max(1, max(len(cv) for cv in covers))
+    a, b = runs[comm.rank]
+    cuda = comm.device.type == "cuda"
+    local = torch.zeros((slots, engine.nnz), dtype=torch.float64,
+                        device=comm.device if cuda else "cpu")
+    if b > a:
+        engine.er_solve(bounds[a], bounds[b], max_cg_iters, cg_tol, blas_threads)
+        for i, (lev, idx) in enumerate(covers[comm.rank]):
+            lo, hi = idx << lev, (idx + 1) << lev
+            # fold the block's 2**lev nodes in tree order (gs_er_scores per node)
+            parts = []
+            for f in range(lo, hi):
+                o = torch.empty(engine.nnz, dtype=torch.float64, device=comm.device) if cuda else None
+                p = engine.er_scores(bounds[f], bounds[f + 1], finalize=False, out=o)
+                parts.append(p if cuda else torch.from_numpy(np.asarray(p)))
+            local[i] = tree_sum(parts)
+    gathered = comm.all_gather_flat(local.reshape(-1)).reshape(comm.world, slots, engine.nnz)
+    level = {}
+    for r, cv in enumerate(covers):
+        for i, key in enumerate(cv):
+            level[key] = gathered[r, i]
+    for lev in range(depth):  # combine siblings bottom-up: the pairwise tree's own order
+        for idx in range((1 << depth) >> (lev + 1)):
+            lk, rk = (lev, 2 * idx), (lev, 2 * idx + 1)
+            if lk in level and rk in level:
+                level[(lev + 1, idx)] = level.pop(lk) + level.pop(rk)
+    return finalize_er(level[(depth, 0)])

@@ -97,6 +97,42 @@ class Engine:
         self.ctx.call("gs_jaccard_part", part, nparts, ptr(o), loc)
         return o
 
+    def jaccard_shares(self, nparts: int):
+        """gs_jaccard_shares: (row_cut, owner_off), nparts + 1 values each -- the
+        owner-pair shares of the sharded Jaccard (the same on every rank)."""
+        rc = np.empty(nparts + 1, dtype=np.int64)
+        oo = np.empty(nparts + 1, dtype=np.int64)
+        self.ctx.call("gs_jaccard_shares", nparts, ptr(rc), ptr(oo))
+        return rc, oo
+
+    def jaccard_part_counts(self, part: int, nparts: int, out=None):
+        """gs_jaccard_part_counts: |N(u) ∩ N(v)| of this part's owner pairs
+        (uint32 numpy array, or the int32/uint32 device tensor ``out``)."""
+        if not 0 <= part < nparts:
+            raise ValueError(f"bad part {part} of {nparts}")
+        _, oo = self.jaccard_shares(nparts)
+        cnt = int(oo[part + 1] - oo[part])
+        if out is None:
+            o, loc = np.empty(cnt, dtype=np.uint32), GS_HOST
+        else:
+            if out.numel() < cnt:
+                raise IndexError(f"counts buffer holds {out.numel()} < {cnt} values")
+            o, loc = out, GS_DEVICE
+        self.ctx.call("gs_jaccard_part_counts", part, nparts, ptr(o), loc)
+        return o
+
+    def jaccard_from_counts(self, nparts: int, counts, stride: int, out=None):
+        """gs_jaccard_from_counts: every part's counts (part p at p * stride) ->
+        the Jaccard score of every CSR entry."""
+        cloc = GS_HOST if isinstance(counts, np.ndarray) else GS_DEVICE
+        if cloc == GS_HOST:
+            counts = np.ascontiguousarray(counts, dtype=np.uint32)
+        if counts.shape[0] < nparts * stride:
+            raise IndexError(f"counts hold {counts.shape[0]} < {nparts} x {stride} values")
+        o, loc = self._out(0, self.nnz, out)
+        self.ctx.call("gs_jaccard_from_counts", nparts, ptr(counts), stride, cloc, ptr(o), loc)
+        return o
+
     def adamic_adar(self, e0: int = 0, e1: int | None = None, out=None, c=None):
         e1 = self.nnz if e1 is None else e1
         if c is None:

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GS_API_VERSION 2
+#define GS_API_VERSION 3
 
 enum {
     GS_OK = 0,
@@ -102,6 +102,26 @@ int gs_jaccard(gs_ctx *ctx, int64_t e0, int64_t e1, double *out, int loc);
  * 0.0 elsewhere, so the element-wise sum of the nparts outputs equals
  * gs_jaccard(0, nnz) bit for bit. */
 int gs_jaccard_part(gs_ctx *ctx, int part, int nparts, double *out, int loc);
+/* Sharded Jaccard with an all-gather of per-pair counts (multi-GPU, SURVEY
+ * 8(e); symmetric graphs, else GS_EUNSUPPORTED).  The owner of an undirected
+ * pair {u, v} is the endpoint of larger degree (ties: smaller id); its CSR
+ * entry (u, v) is the pair's owner entry.  Part p of nparts owns the owner
+ * entries of rows [row_cut[p], row_cut[p+1]) -- contiguous row ranges cut at
+ * equal shares of the intersection work, the same on every rank -- which are
+ * owner entries [owner_off[p], owner_off[p+1]) in CSR order.
+ *   gs_jaccard_shares: row_cut[nparts+1], owner_off[nparts+1] (host; either
+ *     may be NULL).
+ *   gs_jaccard_part_counts: counts[i] = |N(u) ∩ N(v)| of part p's i-th owner
+ *     entry (uint32, owner_off[p+1] - owner_off[p] values).
+ *   gs_jaccard_from_counts: every part's counts (part p's at counts + p*stride,
+ *     e.g. an all-gather of the shares padded to stride) -> out[nnz], the
+ *     score of both CSR entries of every pair (the reference's single fp64
+ *     division of metrics.py:54-59): bit-identical to gs_jaccard(0, nnz).
+ *     A part longer than stride is GS_EINDEX. */
+int gs_jaccard_shares(gs_ctx *ctx, int nparts, int64_t *row_cut, int64_t *owner_off);
+int gs_jaccard_part_counts(gs_ctx *ctx, int part, int nparts, uint32_t *counts, int loc);
+int gs_jaccard_from_counts(gs_ctx *ctx, int nparts, const uint32_t *counts, int64_t stride,
+                           int c_loc, double *out, int loc);
 /* calculate_adamic_adar_scores, metrics.py:67-121 (bit-exact).  c[w] =
  * 1/sqrt(max(log(deg_w+1),1e-10)) as NumPy computes it (metrics.py:104-108),
  * n values. */

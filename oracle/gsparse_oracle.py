@@ -103,6 +103,93 @@ def jaccard(indptr, indices):
     return out
 
 
+def jaccard_counts(indptr, indices):
+    """The integer numerator of metrics.py:46-49: (A_bin @ A_bin)[rows, cols]."""
+    n = len(indptr) - 1
+    ab = sp.csr_matrix((np.ones(len(indices)), indices, indptr), shape=(n, n))
+    inter = ab @ ab
+    rows = csr_rows(indptr)
+    return np.asarray(inter[rows, indices]).ravel().astype(np.int64)
+
+
+def _jac_class(d):
+    """Degree classes of the device's owner-side Jaccard (gs_jaccard.hip)."""
+    d = np.asarray(d, dtype=np.int64)
+    return np.select([d <= 32, d <= 1024, d <= 4096, d <= 8192, d <= 16384],
+                     [-1, 0, 1, 2, 3], default=4)
+
+
+def jaccard_shares(indptr, indices, nparts):
+    """The device's row partition for the sharded Jaccard (gs_jaccard_shares):
+    owner entry = (u, v) with d_u > d_v or (d_u == d_v and u <= v); row work =
+    owned-entry merge (d_u + d_v, rows of degree <= 32) or probe (d_v) work plus
+    d_u per task; R[r] = first row whose exclusive work prefix reaches
+    total * r / P.  Returns (row_cut, owner_off), nparts + 1 values each."""
+    n = len(indptr) - 1
+    indptr = np.asarray(indptr, dtype=np.int64)
+    ix = np.asarray(indices, dtype=np.int64)
+    deg = np.diff(indptr)
+    rows = csr_rows(indptr)
+    du, dv = deg[rows], deg[ix]
+    own = (du > dv) | ((du == dv) & (rows <= ix))
+    k = _jac_class(deg)
+    ew = np.where(k[rows] < 0, du + dv, dv) * own
+    w = np.bincount(rows, weights=ew, minlength=n).astype(np.int64) if n else np.zeros(0, np.int64)
+    # jac_row_tasks: tasks of a row of class k >= 0 with probe work w
+    tab = np.array([2048, 8192, 16384, 32768, 0], dtype=np.int64)[np.maximum(k, 0)]
+    tp = np.maximum(np.maximum(16 * tab, 8 * deg), 65536)
+    nt = np.maximum((w + tp - 1) // tp, (deg + 1023) // 1024)
+    nt = np.where((k >= 0) & (w > 0), np.minimum(nt, deg), 0)
+    work = w + nt * deg
+    S = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(work, out=S[1:])
+    total = int(S[-1])
+    R = [0] + [int(np.searchsorted(S, total * r // nparts, side="left"))
+               for r in range(1, nparts)] + [n]
+    opre = np.zeros(len(ix) + 1, dtype=np.int64)
+    np.cumsum(own, out=opre[1:])
+    O = [int(opre[indptr[r]]) for r in R]
+    return np.array(R, dtype=np.int64), np.array(O, dtype=np.int64)
+
+
+def jaccard_part_counts(indptr, indices, part, nparts):
+    """Counts of part `part`'s owner entries (rows [R[p], R[p+1])) in CSR order."""
+    R, _ = jaccard_shares(indptr, indices, nparts)
+    ip = np.asarray(indptr, dtype=np.int64)
+    ix = np.asarray(indices, dtype=np.int64)
+    rows = csr_rows(ip)
+    deg = np.diff(ip)
+    own = (deg[rows] > deg[ix]) | ((deg[rows] == deg[ix]) & (rows <= ix))
+    sel = own & (rows >= R[part]) & (rows < R[part + 1])
+    return jaccard_counts(ip, ix)[sel].astype(np.uint32)
+
+
+def jaccard_from_counts(indptr, indices, nparts, counts, stride):
+    """Scatter of the parts' counts to both CSR entries of every pair with the
+    reference's single division (metrics.py:54-59)."""
+    R, O = jaccard_shares(indptr, indices, nparts)
+    ip = np.asarray(indptr, dtype=np.int64)
+    ix = np.asarray(indices, dtype=np.int64)
+    n = len(ip) - 1
+    rows = csr_rows(ip)
+    deg = np.diff(ip)
+    own = (deg[rows] > deg[ix]) | ((deg[rows] == deg[ix]) & (rows <= ix))
+    opre = np.concatenate([[0], np.cumsum(own)])
+    part = np.searchsorted(R, rows, side="right") - 1
+    part = np.minimum(part, nparts - 1)
+    e = np.nonzero(own)[0]
+    cnt = np.asarray(counts, dtype=np.float64)[part[e] * stride + (opre[e] - O[part[e]])]
+    uni = deg[rows[e]].astype(np.float64) + deg[ix[e]].astype(np.float64) - cnt
+    val = np.divide(cnt, uni, out=np.zeros_like(cnt), where=uni > 0)
+    # reverse entry (v, u) of each owner entry (u, v): keys sorted in CSR order
+    keys = rows * n + ix
+    rev = np.searchsorted(keys, ix[e] * n + rows[e])
+    out = np.zeros(len(ix), dtype=np.float64)
+    out[e] = val
+    out[rev] = val
+    return out
+
+
 def aa_weights(indptr):
     """metrics.py:100-108: c = 1/sqrt(max(log(deg+1), 1e-10)) with NumPy ufuncs."""
     deg = np.diff(indptr).astype(np.float64)

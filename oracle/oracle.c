@@ -47,6 +47,29 @@ void oracle_jaccard(int64_t n, const int64_t *ip, const int32_t *ix,
     }
 }
 
+/* The same per-edge merge for the entries of rows [r0, r1) only (out indexed by
+ * CSR position): bench.py's bounded CPU-baseline sample on R-MAT graphs. */
+void oracle_jaccard_rows(const int64_t *ip, const int32_t *ix, const int64_t *tp,
+                         const int32_t *ti, int64_t r0, int64_t r1, double *out) {
+    for (int64_t u = r0; u < r1; ++u) {
+        for (int64_t e = ip[u]; e < ip[u + 1]; ++e) {
+            int32_t v = ix[e];
+            int64_t a = ip[u], ae = ip[u + 1], b = tp[v], be = tp[v + 1];
+            int64_t inter = 0;
+            while (a < ae && b < be) {
+                int32_t x = ix[a], y = ti[b];
+                if (x == y) { ++inter; ++a; ++b; }
+                else if (x < y) ++a;
+                else ++b;
+            }
+            double du = (double)(ip[u + 1] - ip[u]);
+            double dv = (double)(ip[v + 1] - ip[v]);
+            double uni = du + dv - (double)inter;
+            out[e] = uni > 0 ? (double)inter / uni : 0.0;
+        }
+    }
+}
+
 /* Adamic-Adar: metrics.py:99-119.
  *   c_w = 1/sqrt(max(log(deg_w+1),1e-10)) (computed by NumPy, passed in);
  *   AA[u,v] = sum over w in out(u) ∩ out(v) of c_w*c_w, accumulated from 0.0

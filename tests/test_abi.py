@@ -52,7 +52,7 @@ def test_ctypes_table_matches_header(built):
 
     assert sorted(_lib.SIGNATURES) == declared_functions()
     L = _lib.lib(built)
-    assert L.gs_api_version() == 2
+    assert L.gs_api_version() == 3
 
 
 def test_library_is_gfx950_code(built):

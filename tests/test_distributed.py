@@ -23,6 +23,18 @@ class OracleEngine:
         self.ip, self.ix, self.d, self.n = ip, ix, d, n
         self.nnz = len(ix)
         self._jac = None
+        rows = O.csr_rows(ip)
+        fwd = np.sort(rows * n + ix)
+        self.symmetric = bool(np.array_equal(fwd, np.sort(ix.astype(np.int64) * n + rows)))
+
+    def jaccard_shares(self, nparts):
+        return O.jaccard_shares(self.ip, self.ix, nparts)
+
+    def jaccard_part_counts(self, part, nparts, out=None):
+        return O.jaccard_part_counts(self.ip, self.ix, part, nparts)
+
+    def jaccard_from_counts(self, nparts, counts, stride, out=None):
+        return O.jaccard_from_counts(self.ip, self.ix, nparts, counts, stride)
 
     def jaccard(self, e0=0, e1=None, out=None):
         if self._jac is None:
@@ -101,8 +113,8 @@ def _worker(rank, world, port, name, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("name", ["karate_csr", "rmat10"])
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("name", ["karate_csr", "rmat10", "roman2000"])
 def test_sharded_equals_single(name, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -123,8 +135,44 @@ def test_sharded_equals_single(name, world):
 
 
 def test_tree_helpers():
-    from gsparse.distributed import edge_ranges, pow2_floor, tree_sum
+    from gsparse.distributed import dyadic_cover, edge_ranges, pow2_floor, tree_sum
 
     assert edge_ranges(10, 3) == [0, 3, 6, 10]
     assert pow2_floor(6) == 4 and pow2_floor(8) == 8 and pow2_floor(1) == 1
     assert tree_sum([1.0, 2.0, 3.0, 4.0]) == (1.0 + 2.0) + (3.0 + 4.0)
+    assert dyadic_cover(0, 32) == [(5, 0)]
+    assert dyadic_cover(5, 11) == [(0, 5), (1, 3), (1, 4), (0, 10)]
+    assert dyadic_cover(3, 3) == []
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 6, 7, 8])
+def test_er_rank_blocks_cover_k(world):
+    """Every rank's columns are whole pairwise-tree nodes and together cover k once."""
+    from gsparse.distributed import dyadic_cover, er_rank_blocks
+
+    for k in (2674, 3210, 2107, 4066, 300, 100):
+        d, b, runs = er_rank_blocks(k, world)
+        assert len(b) == (1 << d) + 1 and b[0] == 0 and b[-1] == k
+        assert runs[0][0] == 0 and runs[-1][1] == len(b) - 1
+        assert all(runs[r][1] == runs[r + 1][0] for r in range(world - 1))
+        for a, z in runs:
+            cov = dyadic_cover(a, z)
+            assert sum(1 << lev for lev, _ in cov) == z - a
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 3, 8])
+@pytest.mark.parametrize("name", ["karate_csr", "rmat10", "roman2000", "star", "triangle"])
+def test_jaccard_count_shares_rebuild_scores(name, nparts):
+    """Owner-pair counts of every part, scattered, are the reference's Jaccard bit for bit."""
+    g = load_golden(name)
+    ip, ix = g["indptr"], g["indices"]
+    R, Oo = O.jaccard_shares(ip, ix, nparts)
+    assert R[0] == 0 and R[-1] == len(ip) - 1 and np.all(np.diff(R) >= 0)
+    parts = [O.jaccard_part_counts(ip, ix, p, nparts) for p in range(nparts)]
+    assert [len(p) for p in parts] == list(np.diff(Oo))
+    stride = max(1, max(len(p) for p in parts))
+    allc = np.zeros(nparts * stride, dtype=np.uint32)
+    for p, c in enumerate(parts):
+        allc[p * stride: p * stride + len(c)] = c
+    got = O.jaccard_from_counts(ip, ix, nparts, allc, stride)
+    assert np.array_equal(got.view(np.uint64), g["scores_jaccard"].view(np.uint64))

@@ -1,0 +1,203 @@
+"""Multi-GPU path on the device.
+
+* The sharded scorers through a real RCCL ("nccl") process group with device
+  tensors -- world 1 here (the test box has one GPU; bench.py's N-rank launch
+  uses the same calls on 8) -- give the single-GPU bits.
+* The Jaccard count shares (gs_jaccard_shares / gs_jaccard_part_counts /
+  gs_jaccard_from_counts) equal the oracle's restatement of the layout and, put
+  back together, the reference's Jaccard bit for bit, on graphs with rows in
+  every owner-side class (LDS tables, bitmap rows, self-loops).
+* Two ranks sharing the GPU over gloo run the whole N = 2 exchange with device
+  compute on both ranks.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+import gsparse_oracle as O
+from conftest import bits_equal, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def gs():
+    import gsparse
+
+    return gsparse
+
+
+def _engine(gs, ei, n):
+    data = gs.Data(edge_index=torch.from_numpy(np.ascontiguousarray(ei)), num_nodes=n)
+    return gs.GraphSparsifier(data, "cuda:0")._engine
+
+
+def _hub_graph():
+    from test_gpu_parity import _hub_graph as hub
+
+    return hub()
+
+
+def _graphs():
+    from gsparse import graphs
+
+    ei, n = _hub_graph()
+    yield "hub", ei, n
+    yield "rmat14", graphs.rmat(14, 8, seed=5), 1 << 14
+    g = load_golden("roman2000")
+    yield "roman2000", g["edge_index"], int(g["num_nodes"])
+    g = load_golden("karate_test")
+    yield "karate_test", g["edge_index"], int(g["num_nodes"])
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 3, 8])
+def test_jaccard_count_shares_vs_oracle(gs, nparts):
+    for name, ei, n in _graphs():
+        ip, ix, _ = O.canonical_csr(ei, n)
+        e = _engine(gs, ei, n)
+        R, Oo = e.jaccard_shares(nparts)
+        Rr, Or = O.jaccard_shares(ip, ix, nparts)
+        assert np.array_equal(R, Rr) and np.array_equal(Oo, Or), name
+        stride = max(1, int(np.diff(Oo).max()))
+        allc = np.zeros(nparts * stride, dtype=np.uint32)
+        dev = torch.zeros(nparts * stride, dtype=torch.int32, device="cuda:0")
+        for p in range(nparts):
+            c = e.jaccard_part_counts(p, nparts)
+            assert np.array_equal(c, O.jaccard_part_counts(ip, ix, p, nparts)), (name, p)
+            allc[p * stride: p * stride + len(c)] = c
+            cnt = int(Oo[p + 1] - Oo[p])
+            e.jaccard_part_counts(p, nparts, out=dev[p * stride: p * stride + max(cnt, 1)])
+        ref = O.jaccard(ip, ix)
+        assert bits_equal(e.jaccard_from_counts(nparts, allc, stride), ref), name
+        out = torch.empty(e.nnz, dtype=torch.float64, device="cuda:0")
+        e.jaccard_from_counts(nparts, dev, stride, out=out)
+        assert bits_equal(out.cpu().numpy(), ref), name
+
+
+def test_jaccard_count_shares_errors(gs):
+    g = load_golden("karate_test")
+    e = _engine(gs, g["edge_index"], int(g["num_nodes"]))
+    _, Oo = e.jaccard_shares(2)
+    stride = int(np.diff(Oo).max())
+    with pytest.raises(IndexError):
+        e.jaccard_from_counts(2, np.zeros(2 * stride, dtype=np.uint32), stride - 1)
+    with pytest.raises(ValueError):
+        e.jaccard_part_counts(2, 2)
+    d = load_golden("directed_dup")
+    ed = _engine(gs, d["edge_index"], int(d["num_nodes"]))
+    assert not ed.symmetric
+    with pytest.raises(NotImplementedError):
+        ed.jaccard_shares(2)
+
+
+@pytest.fixture(scope="module")
+def nccl_world1():
+    """A real RCCL process group of one rank on cuda:0."""
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        yield dist
+    finally:
+        dist.destroy_process_group()
+
+
+def test_nccl_sharded_scorers_equal_single_gpu(gs, nccl_world1):
+    from gsparse import graphs
+    from gsparse.distributed import (Comm, sharded_approx_er, sharded_backbone,
+                                     sharded_edge_scores)
+
+    assert nccl_world1.get_backend() == "nccl"
+    comm = Comm(device=torch.device("cuda", 0))
+    assert comm.device.type == "cuda" and comm.world == 1
+    n = 12000
+    ei = graphs.roman_like(n, 17500, seed=3)
+    data = gs.Data(edge_index=torch.from_numpy(ei), num_nodes=n)
+    sp_ = gs.GraphSparsifier(data, "cuda:0")
+    e = sp_._engine
+    jac = sharded_edge_scores(e, comm, "jaccard")
+    assert jac.is_cuda and bits_equal(jac.cpu().numpy(), e.jaccard())
+    aa = sharded_edge_scores(e, comm, "adamic_adar")
+    assert aa.is_cuda and bits_equal(aa.cpu().numpy(), e.adamic_adar())
+    er = sharded_approx_er(e, comm, epsilon=0.9, max_cg_iters=60, blas_threads=8)
+    assert er.is_cuda
+    single = e.approx_er(epsilon=0.9, max_cg_iters=60, blas_threads=8)
+    assert bits_equal(er.cpu().numpy(), single)
+    cost = sp_._scores_to_cost(e.jaccard(), "jaccard")
+    rows = O.csr_rows(e.indptr())
+    ip, ix, _ = O.canonical_csr(ei, n)
+    pos = np.searchsorted(rows * n + ix, ei[0] * n + ei[1])
+    w = cost[pos]
+    from gsparse.metric_backbone import backbone_mask
+
+    keep = sharded_backbone(comm, ei, n, w)
+    assert np.array_equal(keep, backbone_mask(ei, n, w, 1e-9))
+
+
+def _gloo_rank(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import gsparse
+        from gsparse import graphs
+        from gsparse.distributed import Comm, sharded_approx_er, sharded_edge_scores
+
+        ei, n = _hub_graph()
+        data = gsparse.Data(edge_index=torch.from_numpy(ei), num_nodes=n)
+        e = gsparse.GraphSparsifier(data, "cuda:0")._engine
+        comm = Comm()
+        jac = sharded_edge_scores(e, comm, "jaccard").numpy()
+        n2 = 12000
+        ei2 = graphs.roman_like(n2, 17500, seed=3)
+        e2 = gsparse.GraphSparsifier(gsparse.Data(edge_index=torch.from_numpy(ei2), num_nodes=n2),
+                                     "cuda:0")._engine
+        er = sharded_approx_er(e2, comm, epsilon=0.9, max_cg_iters=60, blas_threads=8).numpy()
+        if rank == 0:
+            q.put((jac, er))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_sharing_the_gpu_over_gloo(gs, world, monkeypatch):
+    """N ranks on the one GPU (device compute on every rank, gloo exchange):
+    Jaccard count shares and ApproxER tree blocks (world 3: the non-power-of-two
+    split) give the single-process bits."""
+    import torch.multiprocessing as mp
+
+    from gsparse import graphs
+
+    monkeypatch.setenv("GSPARSE_REG_SPLIT", "0")  # ranks share the CUs
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    jac, er = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ei, n = _hub_graph()
+    ip, ix, _ = O.canonical_csr(ei, n)
+    assert bits_equal(jac, O.jaccard(ip, ix))
+    n2 = 12000
+    ei2 = graphs.roman_like(n2, 17500, seed=3)
+    e2 = _engine(gs, ei2, n2)
+    assert bits_equal(er, e2.approx_er(epsilon=0.9, max_cg_iters=60, blas_threads=8))

@@ -6,12 +6,14 @@ generators, the JL dimension and the Adamic-Adar weight table -- each
 checked against the reference's golden vectors or its documented answers.
 """
 
+import os
+
 import numpy as np
 import pytest
 import torch
 
 import gsparse_oracle as O
-from conftest import golden_names, load_golden
+from conftest import ROOT, golden_names, load_golden
 from gsparse import graphs
 from gsparse.core import GraphSparsifier
 from gsparse.data import Data
@@ -137,3 +139,50 @@ def test_short_edge_weights_raise_index_error():
     ei = np.array([[0, 1, 1, 2], [1, 0, 2, 1]])
     with pytest.raises(IndexError):
         sharded_backbone(None, ei, 3, np.ones(3), mask_fn=lambda *a, **k: None)
+
+
+def test_default_device_follows_torch_current_device(monkeypatch):
+    """roman_empire_gpu.py:209-213: torch.cuda.set_device(k) then
+    GraphSparsifier(data, device='cpu') -- the context goes to k.  Order:
+    $GSPARSE_DEVICE, torch's current device once CUDA is initialised,
+    $LOCAL_RANK, 0.  (Host logic only; the GPU test does it for real.)"""
+    import torch
+
+    from gsparse import _lib
+
+    monkeypatch.delenv("GSPARSE_DEVICE", raising=False)
+    monkeypatch.delenv("LOCAL_RANK", raising=False)
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: False)
+    assert _lib.default_device() == 0
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 3)
+    assert _lib.default_device() == 3
+    monkeypatch.setenv("LOCAL_RANK", "5")
+    assert _lib.default_device() == 3  # the caller's set_device wins over the launcher's rank
+    monkeypatch.setenv("GSPARSE_DEVICE", "2")
+    assert _lib.default_device() == 2
+
+
+def test_blas_threads_default_is_openblas_count():
+    """The drop-in reproduces the calling process's OpenBLAS thread count."""
+    from threadpoolctl import threadpool_limits
+
+    from gsparse.engine import blas_threads_default
+
+    for t in (1, 3, 16, 64):
+        with threadpool_limits(limits=t, user_api="blas"):
+            assert blas_threads_default() == t
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """bench.py --gpus N starts N ranks itself, and fails loudly when fewer
+    than N GPUs are visible (none here)."""
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "1"], capture_output=True, text=True, timeout=300,
+                       env={k: v for k, v in os.environ.items()
+                            if k not in ("WORLD_SIZE", "GSPARSE_REHEARSE")})
+    assert r.returncode != 0
+    assert "needs 2 GPUs" in (r.stderr + r.stdout)

@@ -3,6 +3,10 @@
 
 usage: pmc_summary.py OUT.json DIR [DIR ...]
 
+The summary's "_meta" records the source hash of the libgsparse sources it
+profiled (tools/provenance.py) and the git HEAD; bench.py refuses to join
+counters whose hash differs from the running tree's.
+
 Each DIR is a rocprofv3 ``-d`` directory of one ``--pmc`` pass; every
 ``*counter_collection.csv`` under it is read.  Output: for each kernel (name
 cut at the argument list), launches and the per-launch mean of each counter
@@ -16,6 +20,9 @@ import json
 import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from provenance import git_head, source_hash  # noqa: E402
 
 
 def short(name: str) -> str:
@@ -42,9 +49,12 @@ def main() -> None:
             h, m = e["TCC_HIT_sum_per_launch"], e["TCC_MISS_sum_per_launch"]
             e["L2_hit_rate"] = round(h / (h + m), 4) if h + m else None
         res[k] = e
+    res["_meta"] = {"source_hash": source_hash(), "git_head": git_head(),
+                    "passes": [os.path.basename(d.rstrip("/")) for d in sys.argv[2:]]}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
-    for k, e in sorted(res.items(), key=lambda kv: -kv[1].get("launches", 0))[:12]:
+    for k, e in sorted(((k, e) for k, e in res.items() if k != "_meta"),
+                       key=lambda kv: -kv[1].get("launches", 0))[:12]:
         print(k[:60], e)
 
 

@@ -2,7 +2,9 @@
 # rocprofv3 summaries of a bench workload (run on the GPU box).
 # Pass 1: kernel trace + stats; passes 2/3: HBM bytes (FETCH_SIZE, WRITE_SIZE)
 # in separate runs (MI355X_MICROARCH.md: TCC slots; FETCH_SIZE reads 1/2 of
-# the bytes of a wide coalesced stream on gfx950); pass 4: L2 hit/miss.
+# the bytes of a wide coalesced stream on gfx950); pass 4: L2 hit/miss; pass 5:
+# SQ issue and wait counters.  The summary carries the sources' hash
+# (tools/provenance.py), which bench.py checks before using it.
 # usage: profile_bench.sh OUTDIR [bench args...]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -19,5 +21,8 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write"
     python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > "$OUT/bench_write.json" 2> "$OUT/write.err" || exit $?
 timeout -k 10 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/l2" -o run -- \
     python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > "$OUT/bench_l2.json" 2> "$OUT/l2.err" || exit $?
-python3 tools/pmc_summary.py "$OUT/pmc_summary.json" "$OUT/fetch" "$OUT/write" "$OUT/l2" > "$OUT/pmc_summary.txt"
+# pass 5: SQ issue / wait counters (bench.py's on_chip fields)
+timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_INSTS_BRANCH --output-format csv -d "$OUT/sq" -o run -- \
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > "$OUT/bench_sq.json" 2> "$OUT/sq.err" || exit $?
+python3 tools/pmc_summary.py "$OUT/pmc_summary.json" "$OUT/fetch" "$OUT/write" "$OUT/l2" "$OUT/sq" > "$OUT/pmc_summary.txt"
 echo "profile done"
