@@ -37,7 +37,17 @@ namespace gs {
 
 static constexpr int kRegThreads = 512;                 // largest workgroup
 static constexpr int kRegMaxChunks = kRegThreads / 32;  // 32 chains per chunk
-static constexpr int kPre = 4;  // slots a thread's ELL row / p_old loads run ahead
+// slots a thread's ELL row / p_old loads run ahead (-DGS_KPRE=: A/B variants,
+// tools/variant_ab.sh)
+#ifndef GS_KPRE
+#define GS_KPRE 1
+#endif
+static constexpr int kPre = GS_KPRE;
+// p_old loads of the p-update pass run this many slots ahead (-DGS_KPRE_P=)
+#ifndef GS_KPRE_P
+#define GS_KPRE_P GS_KPRE
+#endif
+static constexpr int kPreP = GS_KPRE_P;
 
 struct RegArgs {
     int64_t ld, ldn, col0, ncols;

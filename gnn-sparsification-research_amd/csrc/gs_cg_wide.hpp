@@ -473,12 +473,12 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                 for (int u = 0; u < R; ++u)
                     if (valid(u)) pstore(u, r[u]);
             } else {
-                double pb4[R];  // p_old, kPre slots ahead (each slot reads and writes only its row)
+                double pb4[R];  // p_old, kPreP slots ahead (each slot reads and writes only its row)
 #pragma unroll
-                for (int u = 0; u < kPre && u < R; ++u) pb4[u] = pload(u);
+                for (int u = 0; u < kPreP && u < R; ++u) pb4[u] = pload(u);
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
-                    if (u + kPre < R) pb4[u + kPre] = pload(u + kPre);
+                    if (u + kPreP < R) pb4[u + kPreP] = pload(u + kPreP);
                     if (valid(u)) {
                         const double po = pb4[u];
                         if constexpr (!QR) {

@@ -95,20 +95,19 @@ __host__ __device__ __forceinline__ int64_t jac_row_tasks(int k, int64_t du, int
     return nt;
 }
 
-// per row (one wave each): class, task count (work = sum of d_v over owned entries);
-// tot[0..5] = per-class task totals ([kJacClasses]: rows with bitmap tasks),
-// tot[6..10] / tot[11..15] = tasks of rows below r0 / r1 (a part's task range)
+// per row of [r0, r1) (one wave each): class, task count (work = sum of d_v over
+// owned entries); tot[0..4] = per-class task totals of the range, tot[5] = its rows
+// with bitmap tasks.  A part of the sharded form plans only its own rows.
 __global__ void __launch_bounds__(256) k_jac_plan(const int64_t *__restrict__ ip,
-                                                  const int32_t *__restrict__ ix, int64_t n,
-                                                  int64_t r0, int64_t r1,
-                                                  int8_t *__restrict__ cls,
+                                                  const int32_t *__restrict__ ix, int64_t r0,
+                                                  int64_t r1, int8_t *__restrict__ cls,
                                                   int32_t *__restrict__ ntask,
                                                   unsigned long long *__restrict__ tot) {
     const int lane = threadIdx.x & 63;
     const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    unsigned long long mine[3 * kJacClasses + 1] = {};  // lane 0: this wave's task totals
-    for (int64_t u = w0; u < n; u += nw) {
+    unsigned long long mine[kJacClasses + 1] = {};  // lane 0: this wave's task totals
+    for (int64_t u = r0 + w0; u < r1; u += nw) {
         const int64_t a = ip[u], du = ip[u + 1] - a;
         const int k = jac_class(du);
         int64_t w = 0;
@@ -125,28 +124,21 @@ __global__ void __launch_bounds__(256) k_jac_plan(const int64_t *__restrict__ ip
             cls[u] = (int8_t)k;
             ntask[u] = (int32_t)nt;
             if (nt) {
-                const unsigned long long b0 = u < r0 ? 1ull : 0ull, b1 = u < r1 ? 1ull : 0ull;
 #pragma unroll
-                for (int q = 0; q < kJacClasses; ++q) {
-                    const unsigned long long a = q == k ? (unsigned long long)nt : 0ull;
-                    mine[q] += a;
-                    mine[kJacClasses + 1 + q] += a * b0;
-                    mine[2 * kJacClasses + 1 + q] += a * b1;
-                }
+                for (int q = 0; q < kJacClasses; ++q) mine[q] += q == k ? (unsigned long long)nt : 0ull;
                 mine[kJacClasses] += k == kJacBitmap ? 1ull : 0ull;
             }
         }
     }
-    constexpr int NT = 3 * kJacClasses + 1;
-    __shared__ unsigned long long red[NT];
-    if (threadIdx.x < NT) red[threadIdx.x] = 0;
+    __shared__ unsigned long long red[kJacClasses + 1];
+    if (threadIdx.x < kJacClasses + 1) red[threadIdx.x] = 0;
     __syncthreads();
     if (lane == 0)
 #pragma unroll
-        for (int q = 0; q < NT; ++q)
+        for (int q = 0; q <= kJacClasses; ++q)
             if (mine[q]) atomicAdd(&red[q], mine[q]);
     __syncthreads();
-    if (threadIdx.x < NT && red[threadIdx.x]) atomicAdd(&tot[threadIdx.x], red[threadIdx.x]);
+    if (threadIdx.x < kJacClasses + 1 && red[threadIdx.x]) atomicAdd(&tot[threadIdx.x], red[threadIdx.x]);
 }
 
 // Sharded form (gs_jaccard_shares): per-row intersection work of the owner entries
@@ -184,6 +176,25 @@ __global__ void k_jac_owner_flags(const int64_t *__restrict__ ip, const int32_t 
     }
 }
 
+// owner list (sharded form): for owner entry i (CSR order) its CSR position, its
+// reverse entry and d_u + d_v, so the scatter streams them instead of reading
+// both endpoints' indptr at random
+__global__ void k_jac_owner_list(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
+                                 const int32_t *__restrict__ rows, const int64_t *__restrict__ rev,
+                                 const int64_t *__restrict__ opre, int64_t nnz,
+                                 int32_t *__restrict__ opos, int32_t *__restrict__ orev,
+                                 int32_t *__restrict__ osum) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = opre[e];
+        if (opre[e + 1] == i) continue;  // not an owner entry
+        const int32_t u = rows[e], v = ix[e];
+        opos[i] = (int32_t)e;
+        orev[i] = (int32_t)rev[e];
+        osum[i] = (int32_t)((ip[u + 1] - ip[u]) + (ip[v + 1] - ip[v]));
+    }
+}
+
 // cut rows: R[r] = first row u with S[u] >= total * r / P (S: exclusive prefix of the
 // row work, S[n] = total), R[0] = 0, R[P] = n; then E[r] = ip[R[r]] and
 // O[r] = opre[E[r]].  One thread per cut.  out = [R | E | O], 3 (P + 1) values.
@@ -211,7 +222,31 @@ __global__ void k_jac_cuts(const int64_t *__restrict__ S, const int64_t *__restr
     out[2 * (P + 1) + r] = opre[ip[R]];
 }
 
-// sharded form: every part's counts -> both CSR entries of each pair
+// sharded form: every part's counts -> both CSR entries of each pair, one thread per
+// owner pair i; O[0..P] = cuts[2 (P + 1) ..].  fl(d_u + d_v) == d_u + d_v exactly, so
+// the value is jac_value's bit for bit.
+__global__ void k_jac_scatter_owners(const int32_t *__restrict__ opos, const int32_t *__restrict__ orev,
+                                     const int32_t *__restrict__ osum, const int64_t *__restrict__ cuts,
+                                     int P, const uint32_t *__restrict__ cc, int64_t stride,
+                                     int64_t nown, double *__restrict__ out) {
+    const int64_t *O = cuts + 2 * (P + 1);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nown;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int lo = 0, hi = P - 1;  // last part r with O[r] <= i
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (O[mid] <= i) lo = mid;
+            else hi = mid - 1;
+        }
+        const int64_t cnt = cc[lo * stride + (i - O[lo])];
+        const double uni = (double)osum[i] - (double)cnt;
+        const double val = uni > 0.0 ? (double)cnt / uni : 0.0;
+        out[opos[i]] = val;
+        out[orev[i]] = val;
+    }
+}
+
+// sharded form, graphs past int32 positions: every part's counts -> both CSR entries
 __global__ void k_jac_from_counts(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
                                   const int32_t *__restrict__ rows, const int64_t *__restrict__ rev,
                                   const int64_t *__restrict__ opre, const int64_t *__restrict__ cuts,
@@ -231,28 +266,31 @@ __global__ void k_jac_from_counts(const int64_t *__restrict__ ip, const int32_t 
     }
 }
 
+// rows [r0, r1): cnt / gflag indexed u - r0
 __global__ void k_jac_mask(const int8_t *__restrict__ cls, const int32_t *__restrict__ ntask,
-                           int64_t n, int k, int64_t *__restrict__ cnt, int64_t *__restrict__ gflag) {
-    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
+                           int64_t r0, int64_t r1, int k, int64_t *__restrict__ cnt,
+                           int64_t *__restrict__ gflag) {
+    for (int64_t u = r0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < r1;
          u += (int64_t)gridDim.x * blockDim.x) {
         const bool in = cls[u] == k;
-        cnt[u] = in ? ntask[u] : 0;
-        if (gflag) gflag[u] = (in && ntask[u] > 0) ? 1 : 0;
+        cnt[u - r0] = in ? ntask[u] : 0;
+        if (gflag) gflag[u - r0] = (in && ntask[u] > 0) ? 1 : 0;
     }
 }
 
 // tasks of class k in row order; giant rows also get their bitmap slot
 __global__ void k_jac_emit(const int8_t *__restrict__ cls, const int32_t *__restrict__ ntask,
                            const int64_t *__restrict__ off, const int64_t *__restrict__ goff,
-                           int64_t n, int k, int32_t *__restrict__ trow, int32_t *__restrict__ ti,
-                           int32_t *__restrict__ tslot, int32_t *__restrict__ grow) {
-    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
+                           int64_t r0, int64_t r1, int k, int32_t *__restrict__ trow,
+                           int32_t *__restrict__ ti, int32_t *__restrict__ tslot,
+                           int32_t *__restrict__ grow) {
+    for (int64_t u = r0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < r1;
          u += (int64_t)gridDim.x * blockDim.x) {
         if (cls[u] != k) continue;
         const int32_t nt = ntask[u];
         if (!nt) continue;
-        const int64_t o = off[u];
-        const int32_t g = goff ? (int32_t)goff[u] : 0;
+        const int64_t o = off[u - r0];
+        const int32_t g = goff ? (int32_t)goff[u - r0] : 0;
         if (goff) grow[g] = (int32_t)u;
         for (int32_t i = 0; i < nt; ++i) {
             trow[o + i] = (int32_t)u;
@@ -510,6 +548,19 @@ const JacShares &jaccard_shares(gs_ctx *c, int P) {
                                                                          nnz, fl);
         exclusive_scan_i64(c, fl, opre, nnz + 1);
         c->buf("jac_oflag").release();
+        if (nnz < (int64_t)INT32_MAX) {
+            int64_t nown = 0;
+            GS_HIP(hipMemcpyAsync(&nown, opre + nnz, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+            GS_HIP(hipStreamSynchronize(st));
+            const size_t b = sizeof(int32_t) * (size_t)(nown ? nown : 1);
+            auto *opos = (int32_t *)c->buf("jac_opos").ensure(b);
+            auto *orev = (int32_t *)c->buf("jac_orev").ensure(b);
+            auto *osum = (int32_t *)c->buf("jac_osum").ensure(b);
+            if (nnz)
+                k_jac_owner_list<<<grid_for(nnz, 256, 65536), 256, 0, st>>>(
+                    ip, ix, g.rows.as<int32_t>(), g.tpos.as<int64_t>(), opre, nnz, opos, orev, osum);
+            GS_HIP(hipGetLastError());
+        }
     }
     auto *work = (int64_t *)c->buf("jac_work").ensure(sizeof(int64_t) * (n + 1));
     auto *S = (int64_t *)c->buf("jac_wpre").ensure(sizeof(int64_t) * (n + 1));
@@ -567,10 +618,11 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts,
     auto *off = (int64_t *)c->buf("jac_off").ensure(sizeof(int64_t) * (n + 1));
     auto *gfl = (int64_t *)c->buf("jac_gflag").ensure(sizeof(int64_t) * (n + 1));
     auto *goff = (int64_t *)c->buf("jac_goff").ensure(sizeof(int64_t) * (n + 1));
-    constexpr int kTot = 3 * kJacClasses + 1;
+    constexpr int kTot = kJacClasses + 1;
     auto *dtot = (unsigned long long *)c->buf("jac_tot").ensure(8 * kTot);
     GS_HIP(hipMemsetAsync(dtot, 0, 8 * kTot, st));
-    k_jac_plan<<<grid_for(n, 4, 4096), 256, 0, st>>>(ip, ix, n, r0, r1, cls, ntask, dtot);
+    const int64_t nr = r1 - r0;  // this part's rows: planned, task lists emitted
+    if (nr) k_jac_plan<<<grid_for(nr, 4, 4096), 256, 0, st>>>(ip, ix, r0, r1, cls, ntask, dtot);
     if (e1 > e0)
         k_jac_light<<<grid_for(e1 - e0, 256, 65536), 256, 0, st>>>(ip, ix, g.rows.as<int32_t>(), e0,
                                                                    e1, sk);
@@ -603,22 +655,22 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts,
         const bool giant = k == kJacBitmap;
         const int64_t ntot = (int64_t)htot[k], ngiant = giant ? (int64_t)htot[kJacClasses] : 0;
         if (!ntot) continue;
-        GS_HIP(hipMemsetAsync(cnt + n, 0, sizeof(int64_t), st));
-        GS_HIP(hipMemsetAsync(gfl + n, 0, sizeof(int64_t), st));
-        k_jac_mask<<<grid_for(n, 256, 16384), 256, 0, st>>>(cls, ntask, n, k, cnt,
-                                                            giant ? gfl : nullptr);
-        exclusive_scan_i64(c, cnt, off, n + 1);
-        if (giant) exclusive_scan_i64(c, gfl, goff, n + 1);
+        GS_HIP(hipMemsetAsync(cnt + nr, 0, sizeof(int64_t), st));
+        GS_HIP(hipMemsetAsync(gfl + nr, 0, sizeof(int64_t), st));
+        k_jac_mask<<<grid_for(nr, 256, 16384), 256, 0, st>>>(cls, ntask, r0, r1, k, cnt,
+                                                             giant ? gfl : nullptr);
+        exclusive_scan_i64(c, cnt, off, nr + 1);
+        if (giant) exclusive_scan_i64(c, gfl, goff, nr + 1);
         int32_t *tslot = giant ? (int32_t *)c->buf("jac_tslot").ensure(sizeof(int32_t) * ntot)
                                : nullptr;
         int32_t *grow = giant ? (int32_t *)c->buf("jac_grow").ensure(sizeof(int32_t) * ngiant)
                               : nullptr;
-        k_jac_emit<<<grid_for(n, 256, 16384), 256, 0, st>>>(cls, ntask, off, giant ? goff : nullptr,
-                                                            n, k, trow, ti, tslot, grow);
+        k_jac_emit<<<grid_for(nr, 256, 16384), 256, 0, st>>>(cls, ntask, off, giant ? goff : nullptr,
+                                                             r0, r1, k, trow, ti, tslot, grow);
         GS_HIP(hipGetLastError());
         GS_CHECK(ntot <= INT32_MAX, GS_EUNSUPPORTED, "too many Jaccard tasks (%lld)", (long long)ntot);
-        // this part's rows' tasks (tasks are emitted in row order)
-        const int64_t tlo = (int64_t)htot[kJacClasses + 1 + k], thi = (int64_t)htot[2 * kJacClasses + 1 + k];
+        // every emitted task is this part's (only its rows were planned)
+        const int64_t tlo = 0, thi = ntot;
         const unsigned nb = (unsigned)(thi - tlo);
         if (k < kJacBitmap && !nb) continue;
         // hash classes: on side stream k once the task lists are emitted
@@ -650,9 +702,9 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts,
                 const int64_t g1 = g0 + per < ngiant ? g0 + per : ngiant;
                 // task range of rows hrow[g0 .. g1): tasks are in row order
                 int64_t tb[2];
-                GS_HIP(hipMemcpyAsync(&tb[0], off + hrow[g0], 8, hipMemcpyDeviceToHost, st));
+                GS_HIP(hipMemcpyAsync(&tb[0], off + (hrow[g0] - r0), 8, hipMemcpyDeviceToHost, st));
                 if (g1 < ngiant)
-                    GS_HIP(hipMemcpyAsync(&tb[1], off + hrow[g1], 8, hipMemcpyDeviceToHost, st));
+                    GS_HIP(hipMemcpyAsync(&tb[1], off + (hrow[g1] - r0), 8, hipMemcpyDeviceToHost, st));
                 GS_HIP(hipStreamSynchronize(st));
                 if (g1 >= ngiant) tb[1] = ntot;
                 // this part's tasks only
@@ -694,13 +746,22 @@ void jaccard_from_counts(gs_ctx *c, int P, const uint32_t *cc, int64_t stride, d
     GS_HIP(hipMemcpyAsync(dcut, sh.cuts.data(), sizeof(int64_t) * sh.cuts.size(),
                           hipMemcpyHostToDevice, c->stream));
     hipEvent_t t0 = prof_begin(c);
-    k_jac_from_counts<<<grid_for(nnz, 256, 65536), 256, 0, c->stream>>>(
-        g.indptr.as<int64_t>(), g.indices.as<int32_t>(), g.rows.as<int32_t>(), g.tpos.as<int64_t>(),
-        c->buf("jac_opre").as<int64_t>(), dcut, P, cc, stride, nnz, out);
-    GS_HIP(hipGetLastError());
-    // reads rows, ix, opre, the endpoints' indptr and the counts; writes both entries
-    prof_end(c, t0, "jaccard_scatter", (double)nnz * (4.0 + 4.0 + 8.0 + 32.0) + 8.0 * (double)nnz +
-                                           2.0 * (double)sh.O(P));
+    const int64_t nown = sh.O(P);
+    if (nnz < (int64_t)INT32_MAX) {
+        // per owner pair: position, reverse position, d_u + d_v, the count (4 B each) in;
+        // both entries (8 B each) out
+        k_jac_scatter_owners<<<grid_for(nown, 256, 65536), 256, 0, c->stream>>>(
+            c->buf("jac_opos").as<int32_t>(), c->buf("jac_orev").as<int32_t>(),
+            c->buf("jac_osum").as<int32_t>(), dcut, P, cc, stride, nown, out);
+        GS_HIP(hipGetLastError());
+        prof_end(c, t0, "jaccard_scatter", 32.0 * (double)nown);
+    } else {
+        k_jac_from_counts<<<grid_for(nnz, 256, 65536), 256, 0, c->stream>>>(
+            g.indptr.as<int64_t>(), g.indices.as<int32_t>(), g.rows.as<int32_t>(), g.tpos.as<int64_t>(),
+            c->buf("jac_opre").as<int64_t>(), dcut, P, cc, stride, nnz, out);
+        GS_HIP(hipGetLastError());
+        prof_end(c, t0, "jaccard_scatter", 48.0 * (double)nnz + 8.0 * (double)nown);
+    }
     // the host copy of cuts must outlive the async H2D copy: it lives in the cache
 }
 

@@ -13,6 +13,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
                                 "gnn-sparsification-research_amd"))
 import gsparse  # noqa: E402
 from gsparse import graphs  # noqa: E402
+from gsparse.engine import blas_threads_default  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from provenance import source_hash  # noqa: E402
 
 ei, n = graphs.roman_like(), 22_662
 data = gsparse.Data(edge_index=torch.from_numpy(ei), num_nodes=n)
@@ -30,5 +34,6 @@ for rep in range(2):  # the first pass includes context creation and code loadin
     out = {"init_s": round(t_init, 4), "jaccard_s": round(t_jac, 4), "approx_er_s": round(t_er, 4),
            "total_s": round(t_init + t_jac + t_er, 4),
            "scored_edges_per_s": round(ei.shape[1] / (t_init + t_jac + t_er), 1),
-           "checksum": [float(np.sum(jac)), float(np.sum(er))]}
+           "checksum": [float(np.sum(jac)), float(np.sum(er))],
+           "blas_threads_order": blas_threads_default(), "source_hash": source_hash()}
 print(json.dumps(out))
