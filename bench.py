@@ -138,12 +138,18 @@ def make_roofline(name: str, avg_ms: float, bytes_per: float, launches: int, wor
     cyc = avg_ms * 1e-3 * CLOCK_GHZ * 1e9 * CU_COUNT  # CU-cycles of one launch
     oc = {}
     if "SQ_INSTS_LDS" in ctr:
-        oc["lds_issue_frac"] = round(ctr["SQ_INSTS_LDS"] / cyc, 4)  # <= 1 LDS instruction / CU / clk
+        # LDS array cycles: 2 per conflict-free ds_read_b64 wave-instruction (the
+        # kernels' dominant LDS op; MI355X_MICROARCH.md LDS table) + the measured
+        # bank-conflict cycles, against one LDS array per CU
+        busy = 2.0 * ctr["SQ_INSTS_LDS"] + ctr.get("SQ_LDS_BANK_CONFLICT", 0.0)
+        oc["lds_busy_frac"] = round(busy / cyc, 4)
     if "SQ_INSTS_VALU" in ctr:
         oc["valu_issue_frac"] = round(ctr["SQ_INSTS_VALU"] / (4 * cyc), 4)  # 4 SIMDs per CU
     if "SQ_WAIT_ANY" in ctr and ctr.get("SQ_WAVE_CYCLES"):
         oc["wave_wait_frac"] = round(ctr["SQ_WAIT_ANY"] / ctr["SQ_WAVE_CYCLES"], 4)
     if oc:
+        # the nearest on-chip throughput bound (LDS array or VALU issue)
+        oc["frac"] = max(oc.get("lds_busy_frac", 0.0), oc.get("valu_issue_frac", 0.0))
         oc["source"] = src
         roof["on_chip"] = oc
     return roof

@@ -48,6 +48,9 @@ static constexpr int kPre = GS_KPRE;
 #define GS_KPRE_P GS_KPRE
 #endif
 static constexpr int kPreP = GS_KPRE_P;
+// the one-wave form (k_cg_regres, hand-pipelined gathers) keeps its own, validated
+// distance: at 1 slot its results were wrong (tests m5-narrow, round 3)
+static constexpr int kPreN = 4;
 
 struct RegArgs {
     int64_t ld, ldn, col0, ncols;
@@ -457,12 +460,12 @@ __global__ void __launch_bounds__(NT) k_cg_regres(RegArgs A) {
             {
                 launder();
                 double acc = 0.0;
-                uint4 eb[R];  // ELL rows and lengths, kPre slots ahead
+                uint4 eb[R];  // ELL rows and lengths, kPreN slots ahead
                 int lb[R];
                 double pw[R];     // own p, two slots ahead
                 double pg[R][8];  // gathers, one slot ahead
 #pragma unroll
-                for (int u = 0; u < kPre && u < R; ++u) {
+                for (int u = 0; u < kPreN && u < R; ++u) {
                     eb[u] = ell_row(u);
                     lb[u] = len_row(u);
                 }
@@ -471,9 +474,9 @@ __global__ void __launch_bounds__(NT) k_cg_regres(RegArgs A) {
                 spmv_issue(eb[0], lb[0], pw[0], pg[0], 0);
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
-                    if (u + kPre < R) {
-                        eb[u + kPre] = ell_row(u + kPre);
-                        lb[u + kPre] = len_row(u + kPre);
+                    if (u + kPreN < R) {
+                        eb[u + kPreN] = ell_row(u + kPreN);
+                        lb[u + kPreN] = len_row(u + kPreN);
                     }
                     if (u + 2 < R) pw[u + 2] = valid(u + 2) ? ldc(slot_code(u + 2)) : 0.0;
                     if (u + 1 < R) spmv_issue(eb[u + 1], lb[u + 1], pw[u + 1], pg[u + 1], (u + 1) & 1);
@@ -503,7 +506,7 @@ __global__ void __launch_bounds__(NT) k_cg_regres(RegArgs A) {
                 double pw[R];
                 double pg[R][8];
 #pragma unroll
-                for (int u = 0; u < kPre && u < R; ++u) {
+                for (int u = 0; u < kPreN && u < R; ++u) {
                     eb[u] = ell_row(u);
                     lb[u] = len_row(u);
                 }
@@ -512,9 +515,9 @@ __global__ void __launch_bounds__(NT) k_cg_regres(RegArgs A) {
                 spmv_issue(eb[0], lb[0], pw[0], pg[0], 0);
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
-                    if (u + kPre < R) {
-                        eb[u + kPre] = ell_row(u + kPre);
-                        lb[u + kPre] = len_row(u + kPre);
+                    if (u + kPreN < R) {
+                        eb[u + kPreN] = ell_row(u + kPreN);
+                        lb[u + kPreN] = len_row(u + kPreN);
                     }
                     if (u + 2 < R) pw[u + 2] = (UNIT && valid(u + 2)) ? ldc(slot_code(u + 2)) : 0.0;
                     if (u + 1 < R) spmv_issue(eb[u + 1], lb[u + 1], pw[u + 1], pg[u + 1], (u + 1) & 1);

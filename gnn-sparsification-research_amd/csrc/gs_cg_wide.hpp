@@ -458,6 +458,9 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             launder();
             // slots u < ulds: p at lds0 + 256 G u (their stores need no valid test either:
             // a lane's LDS-prefix rows are its own chain rows or its chunk's)
+            // (tried, round 3: the global p rows' loads without the VMEM drain, or
+            // branch-free with a select -- 43.85 / 43.70 vs 43.81 us per column-iteration,
+            // profiles/r03e/: the drain is not what the p pass waits on)
             auto pload = [&](int u) -> double {
                 return u < ulds ? lds_at(lds0() + 256u * G * u) : valid(u) ? ldc(code_of(rowof(u))) : 0.0;
             };
