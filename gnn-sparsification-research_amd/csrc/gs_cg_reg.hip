@@ -139,10 +139,23 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     int64_t keep[kRegMaxChunks], lbase[kRegMaxChunks], tot = 0;
     for (int t = 0; t < T; ++t) tot += hlen[t];
     const int64_t align = 32 * G;
-    for (int t = 0; t < T; ++t) {
-        keep[t] = tot <= cap ? hlen[t] : (cap * hlen[t] / tot) / align * align;
-        if (const char *e = getenv("GSPARSE_REG_KEEP")) keep[t] = std::min<int64_t>(keep[t], atoll(e));
+    for (int t = 0; t < T; ++t) keep[t] = tot <= cap ? hlen[t] : (cap * hlen[t] / tot) / align * align;
+    if (tot > cap) {
+        // the capacity the rounding left: one more wave-slot each for the chunks with the
+        // most rows outside LDS (Roman, 8 chunks: 7 x 64 more rows in LDS)
+        int64_t left = cap;
+        for (int t = 0; t < T; ++t) left -= keep[t];
+        while (left >= align) {
+            int best = -1;
+            for (int t = 0; t < T; ++t)
+                if (keep[t] + align <= hlen[t] && (best < 0 || hlen[t] - keep[t] > hlen[best] - keep[best])) best = t;
+            if (best < 0) break;
+            keep[best] += align;
+            left -= align;
+        }
     }
+    if (const char *e = getenv("GSPARSE_REG_KEEP"))
+        for (int t = 0; t < T; ++t) keep[t] = std::min<int64_t>(keep[t], atoll(e));
     int64_t zs = 0;
     for (int t = 0; t < T; ++t) {
         lbase[t] = zs;

@@ -479,6 +479,44 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                 double pb4[R];  // p_old, kPreP slots ahead (each slot reads and writes only its row)
 #pragma unroll
                 for (int u = 0; u < kPreP && u < R; ++u) pb4[u] = pload(u);
+                if constexpr (!SPLIT) {
+                    // two straight-line passes: every slot reads p_old from LDS (slots past
+                    // the wave's LDS prefix read the zero slot and store to the scratch
+                    // slot: x += alpha * 0 and p to scratch change nothing), then the slots
+                    // past the prefix redo their update from the global p rows.  No branch
+                    // between a prefetch and its use, so the waits count only what is needed.
+                    const uint32_t zaddr = (uint32_t)zslot * 8u, saddr = (uint32_t)(zslot + 1) * 8u;  // the scratch slot
+                    double pf[R];
+#pragma unroll
+                    for (int u = 0; u < kPreP && u < R; ++u) pf[u] = lds_at(u < ulds ? lds0() + 256u * G * u : zaddr);
+#pragma unroll
+                    for (int u = 0; u < R; ++u) {
+                        if (u + kPreP < R)
+                            pf[u + kPreP] = lds_at(u + kPreP < ulds ? lds0() + 256u * G * (u + kPreP) : zaddr);
+                        const double po = pf[u];
+                        if constexpr (!QR) {
+                            const double t1 = alpha_prev * po;
+                            x[u] = x[u] + t1;
+                            asm volatile("" : "+v"(x[u]));  // now, not deferred to the second pass
+                        }
+                        const double pb = po * beta;
+                        lds_put(u < ulds && valid(u) ? lds0() + 256u * G * u : saddr, pb + r[u]);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    launder();
+#pragma unroll
+                    for (int u = 0; u < R; ++u) {
+                        if (u >= ulds && valid(u)) {
+                            const double po = ldc(code_of(rowof(u)));
+                            if constexpr (!QR) {
+                                const double t1 = alpha_prev * po;
+                                x[u] = x[u] + t1;
+                            }
+                            const double pb = po * beta;
+                            pstore(u, pb + r[u]);
+                        }
+                    }
+                } else
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
                     if (u + kPreP < R) pb4[u + kPreP] = pload(u + kPreP);
