@@ -1008,12 +1008,16 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = ctx.profile_read()
     ctx.profile(False)
+    rank_ms = None
     if dist:
+        # every rank's own time (the step time is the slowest rank's)
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         if dist.get_backend() != "nccl":
             t = t.cpu()
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        allt = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        rank_ms = [round(float(x.item()) * 1e3 / args.steps, 2) for x in allt]
+        elapsed = max(float(x.item()) for x in allt)
     ms_per_step = elapsed * 1e3 / args.steps
     value = E * args.steps / elapsed  # every step scores all E edges (with both metrics)
 
@@ -1046,6 +1050,8 @@ def main():
         "roofline": roofline,
         "kernels": kernels,
     }
+    if rank_ms is not None:
+        result["rank_ms_per_step"] = rank_ms
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # one BLAS thread: the fastest setting for this SciPy CG (n=22,662) on
         # the hosts measured (8 threads: 3.8x slower from ddot threading overhead)
