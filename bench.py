@@ -44,6 +44,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # no fp64 figure); a register-only v_mfma_f64_16x16x4_f64 loop sustains 49-50 on the
 # box (tools/mfma_f64_peak.hip, profiles/r01j_mfma_f64_peak.log).
 FP64_MFMA_PEAK_TFS = 78.6
+# fp64 VECTOR peak without contraction: 78.6 TFLOP/s counts an FMA as 2 flops; the CG
+# must not contract (SciPy's separately rounded products), so its arithmetic roof is
+# one fp64 op per lane-slot: 16 fp64 lanes per SIMD per clock x 1024 SIMDs x 2.4 GHz
+FP64_VALU_PEAK_TFS = 39.3
+SIMDS_PER_CU = 4
 
 
 # profiler name -> kernel symbol prefix in the rocprofv3 summaries; "jaccard"
@@ -106,7 +111,7 @@ def kernel_counters(summ: dict, name: str):
 
 
 def make_roofline(name: str, avg_ms: float, bytes_per: float, launches: int, workload: str,
-                  world: int) -> dict:
+                  world: int, flops_per: float | None = None) -> dict:
     """Roofline of the dominant kernel.  Headline (`achieved`, `frac`): measured
     HBM-side traffic -- rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per call of the same
     sources (FETCH_SIZE counts half of a wide stream on gfx950, WRITE_SIZE is exact:
@@ -114,7 +119,12 @@ def make_roofline(name: str, avg_ms: float, bytes_per: float, launches: int, wor
     kernel can reach.  `algorithmic`: SURVEY 8(d)'s bytes over the same time (above
     1 when the working set is re-read from LDS, registers or the Infinity Cache
     instead of HBM).  `on_chip`: issue rates from the SQ counters of the same
-    summary (LDS / VALU instructions per CU-cycle, wave time spent waiting)."""
+    summary (LDS array busy, VALU busy per SIMD, wave time spent waiting).
+
+    `flops_per` (the CG solvers: SURVEY 8(d)'s SciPy operation count, 2 nnz(L_reg)
+    + 12 n flops per column-iteration) makes the fp64 arithmetic roof the headline:
+    those kernels keep r, x, p on chip by design, so HBM is not what bounds them
+    (the measured HBM fraction stays, under `hbm`)."""
     alg = bytes_per / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     roof = {"kernel": name, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": None, "traffic": None, "avg_launch_ms": round(avg_ms, 5), "launches": launches,
@@ -123,14 +133,31 @@ def make_roofline(name: str, avg_ms: float, bytes_per: float, launches: int, wor
             "algorithmic": {"bytes_per_launch": bytes_per, "achieved": round(alg, 1),
                             "frac": round(alg / HBM_PEAK_GBS, 4),
                             "note": "SURVEY 8(d) algorithmic bytes; may exceed 1 (reuse on chip)"}}
+    def fp64_headline(r, oc):
+        # headline: the fp64 arithmetic roof; measured HBM traffic is the secondary view
+        if not flops_per:
+            return r
+        tfs = flops_per / (avg_ms * 1e-3) / 1e12
+        oc.update(fp64_tflops=round(tfs, 3), fp64_frac=round(tfs / FP64_VALU_PEAK_TFS, 4),
+                  flops_per_launch=flops_per)
+        r["hbm"] = {"achieved": r["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": r["frac"], "basis": r["basis"]}
+        r.update(bound="fp64-valu", achieved=oc["fp64_tflops"], peak=FP64_VALU_PEAK_TFS,
+                 unit="TFLOP/s", frac=oc["fp64_frac"],
+                 basis="SURVEY 8(d) SciPy CG operation count (2 nnz(L_reg) + 12 n flops per "
+                       "column-iteration) / live HIP-event launch time, against the fp64 VALU "
+                       "peak without contraction")
+        r.setdefault("on_chip", oc)
+        return r
+
     if world > 1:  # the committed summaries are of 1-GPU runs (a rank launches a share)
         roof["basis"] = "no PMC at N > 1 (summaries are 1-GPU runs); see algorithmic"
-        return roof
+        return fp64_headline(roof, {})
     summ, src, note = pmc_summary(workload)
     ctr = kernel_counters(summ, name) if summ else None
     if ctr is None or "FETCH_SIZE_KB" not in ctr or "WRITE_SIZE_KB" not in ctr:
         roof["basis"] = f"no counters for {name}: {note or src}; see algorithmic"
-        return roof
+        return fp64_headline(roof, {})
     traffic = (2.0 * ctr["FETCH_SIZE_KB"] + ctr["WRITE_SIZE_KB"]) * 1024.0
     gbps = traffic / (avg_ms * 1e-3) / 1e9
     roof.update(achieved=round(gbps, 1), frac=round(gbps / HBM_PEAK_GBS, 4), traffic=round(traffic),
@@ -143,15 +170,24 @@ def make_roofline(name: str, avg_ms: float, bytes_per: float, launches: int, wor
         # bank-conflict cycles, against one LDS array per CU
         busy = 2.0 * ctr["SQ_INSTS_LDS"] + ctr.get("SQ_LDS_BANK_CONFLICT", 0.0)
         oc["lds_busy_frac"] = round(busy / cyc, 4)
+    if "SQ_ACTIVE_INST_VALU" in ctr:
+        # VALU busy: SQ_ACTIVE_INST_VALU counts quad-cycles (summed over waves) in which a
+        # wave executes VALU; a SIMD executes one wave's VALU at a time, so the bound is
+        # the SIMDs' quad-cycles, 4 SIMDs per CU x CU-cycles / 4 (MI355X_MICROARCH.md
+        # constants table: SQ_* count quad-cycles)
+        oc["valu_busy_frac"] = round(ctr["SQ_ACTIVE_INST_VALU"] / (SIMDS_PER_CU * cyc / 4.0), 4)
     if "SQ_INSTS_VALU" in ctr:
-        oc["valu_issue_frac"] = round(ctr["SQ_INSTS_VALU"] / (4 * cyc), 4)  # 4 SIMDs per CU
+        oc["valu_insts_per_launch"] = ctr["SQ_INSTS_VALU"]
     if "SQ_WAIT_ANY" in ctr and ctr.get("SQ_WAVE_CYCLES"):
         oc["wave_wait_frac"] = round(ctr["SQ_WAIT_ANY"] / ctr["SQ_WAVE_CYCLES"], 4)
     if oc:
-        # the nearest on-chip throughput bound (LDS array or VALU issue)
-        oc["frac"] = max(oc.get("lds_busy_frac", 0.0), oc.get("valu_issue_frac", 0.0))
         oc["source"] = src
         roof["on_chip"] = oc
+    fp64_headline(roof, oc)
+    if oc:
+        # the nearest on-chip throughput bound (LDS array, VALU issue, fp64 arithmetic)
+        oc["frac"] = max(oc.get("lds_busy_frac", 0.0), oc.get("valu_busy_frac", 0.0),
+                         oc.get("fp64_frac", 0.0))
     return roof
 
 
@@ -884,6 +920,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="roman", choices=["roman", "rmat", "arxiv", "backbone", "exact_er", "topology", "geodesic", "scorers"])
     ap.add_argument("--scale", type=int, default=22, help="R-MAT scale for --workload rmat")
+    ap.add_argument("--keep", type=float, default=0.5,
+                    help="--workload rmat: retention ratio of the global top-k in the step "
+                         "(Jaccard-T; 1.0 = scores only)")
     ap.add_argument("--bb-graph", default="rmat", choices=["rmat", "roman"],
                     help="graph of --workload backbone (R-MAT at --bb-scale, or Roman-like)")
     ap.add_argument("--bb-scale", type=int, default=18)
@@ -893,6 +932,8 @@ def main():
                     help="OpenBLAS ddot order to reproduce (reference run with this many threads)")
     ap.add_argument("--rng", default=os.environ.get("GSPARSE_ER_RNG", "device"),
                     choices=["host", "device"])
+    ap.add_argument("--box-order-steps", type=int, default=2,
+                    help="steps timed again in this box's default OpenBLAS order (secondary)")
     ap.add_argument("--cpu-sample-cols", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -931,7 +972,7 @@ def main():
 
     from gsparse import graphs
     from gsparse._lib import Context
-    from gsparse.distributed import Comm, sharded_approx_er, sharded_edge_scores
+    from gsparse.distributed import Comm, sharded_approx_er, sharded_edge_scores, sharded_sparsify
     from gsparse.engine import Engine, jl_dim
 
     if args.workload == "backbone":
@@ -973,13 +1014,40 @@ def main():
     jac_out = torch.empty(nnz, dtype=torch.float64, device=dev)
     er_out = torch.empty(nnz, dtype=torch.float64, device=dev)
 
+    er_cols = None
+    if world > 1 and with_er:
+        from gsparse.distributed import er_rank_blocks
+
+        _, eb, runs = er_rank_blocks(k, world)
+        a_, b_ = runs[rank]
+        er_cols = (eb[a_], eb[b_]) if b_ > a_ else (0, 0)
+
+    # configs[3] "Jaccard-T": the global top-k of the scores (core.py:229-240) is part of
+    # the R-MAT step, on every rank after the all-gather (device tie rule)
+    with_topk = args.workload == "rmat" and args.keep < 1.0
+    mask_out = torch.empty(E, dtype=torch.uint8, device=dev) if with_topk else None
+    sel_info = {}
+
+    def select(scores):
+        if world > 1:
+            _, info = sharded_sparsify(eng, comm, scores, E, args.keep, tie_break="stable",
+                                       out=mask_out)
+        else:
+            _, cut, nb, nt = eng.topk_mask(scores, E, int(E * args.keep), False, out=mask_out)
+            info = {"cut": cut, "beyond": nb, "tied": nt}
+        sel_info.update(info)
+
     def step():
         if world > 1:
             jac = sharded_edge_scores(eng, comm, "jaccard", bounds=bounds, out=jac_out)
+            if with_topk:
+                select(jac)
             er = sharded_approx_er(eng, comm, blas_threads=args.blas_threads,
                                    rng_mode=args.rng) if with_er else None
             return jac, er
         eng.jaccard(0, nnz, out=jac_out)
+        if with_topk:
+            select(jac_out)
         if with_er:
             rng = np.random.default_rng(42)
             eng.er_prepare(k)
@@ -1025,12 +1093,24 @@ def main():
     roofline = None
     if prof:
         name, p = max(((k, v) for k, v in prof.items() if v["ms"] > 0), key=lambda kv: kv[1]["ms"])
+        flops = None
+        if with_er and name in ("cg_reg", "cg_res"):
+            # SciPy's CG does 2 nnz(L_reg) (SpMV) + 3 x 2n (dots) + 3 x 2n
+            # (updates) flops per column-iteration; this rank's columns, their iterations
+            c0, c1 = er_cols if er_cols else (0, k)
+            its = float(eng.er_iterations()[c0:c1].astype(np.int64).sum())
+            ip_h, ix_h, _ = ctx.csr()
+            loops = int((np.repeat(np.arange(n), np.diff(ip_h)) == ix_h).sum())
+            lnnz = nnz - loops + n  # L_reg = diag(deg) - A + 1e-6 I: every diagonal stored
+            flops = (2.0 * lnnz + 12.0 * n) * its
         roofline = make_roofline(name, p["ms"] / p["launches"], p["bytes"] / p["launches"],
-                                 p["launches"], args.workload, world)
+                                 p["launches"], args.workload, world, flops_per=flops)
     kernels = {k2: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k2, v in prof.items()}
 
     result = {
-        "metric": "scored edges/sec (Jaccard+ApproxER)" if with_er else "scored edges/sec (Jaccard)",
+        "metric": "scored edges/sec (Jaccard+ApproxER)" if with_er else
+                  ("scored edges/sec (Jaccard-T: scores + global top-k)" if with_topk
+                   else "scored edges/sec (Jaccard)"),
         "value": round(value, 1),
         "unit": "scored edges/s",
         "n_gpus": world,
@@ -1046,12 +1126,38 @@ def main():
                    "cg_maxiter": 500 if with_er else None,
                    "blas_threads_order": args.blas_threads, "rng": args.rng,
                    "parallelism": f"edges+jl-columns/{world}" if world > 1 else "1 GPU",
+                   "topk": ({"keep": args.keep, "num_keep": int(E * args.keep), "tie_rule": "device (stable)",
+                             "tied_at_cut": sel_info.get("tied"), "beyond_cut": sel_info.get("beyond")}
+                            if with_topk else None),
                    "graph_gen_s": round(t_gen, 2)},
         "roofline": roofline,
         "kernels": kernels,
     }
     if rank_ms is not None:
         result["rank_ms_per_step"] = rank_ms
+    if with_er and world == 1 and args.box_order_steps > 0:
+        # secondary figure (not `value`): the same step in the OpenBLAS ddot order the
+        # drop-in API reproduces by default on this box (threadpoolctl's thread count:
+        # what the reference run here would use), beside the headline's fixed order
+        from gsparse.engine import blas_threads_default
+
+        bt_box = blas_threads_default()
+        if bt_box != args.blas_threads:
+            bt_main = args.blas_threads
+            args.blas_threads = bt_box
+            step()
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            for _ in range(args.box_order_steps):
+                step()
+            torch.cuda.synchronize(dev)
+            ms_box = (time.perf_counter() - t1) * 1e3 / args.box_order_steps
+            args.blas_threads = bt_main
+        else:
+            ms_box = ms_per_step
+        result["box_blas_order"] = {"blas_threads": bt_box, "ms_per_step": round(ms_box, 2),
+                                    "value": round(E / (ms_box * 1e-3), 1),
+                                    "note": "secondary: the drop-in default order on this box"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # one BLAS thread: the fastest setting for this SciPy CG (n=22,662) on
         # the hosts measured (8 threads: 3.8x slower from ddot threading overhead)

@@ -225,6 +225,8 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     GS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
     int P = 0;
     int64_t W = ncols;  // columns solved whole (the first W), the rest split
+    split_abort_poll(c, false);
+    if (c->reg_split_off && c->reg_split_off_epoch != c->g.epoch) c->reg_split_off = false;  // new graph
     if (NT == 512 && T >= 2 && ncols > 0 && !c->reg_split_off) {
         const char *se = getenv("GSPARSE_REG_SPLIT");
         const int forced = se ? atoi(se) : -1;
@@ -348,9 +350,12 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     }
     auto *dpt = (int32_t *)c->buf("er_reg_split_ptab").ensure(sizeof(hpt));
     auto *dtab = (int64_t *)c->buf("er_reg_split_tab").ensure(sizeof(htab));
-    // stream-ordered copies; hpt / htab outlive them (the stream is synchronised below)
-    GS_HIP(hipMemcpyAsync(dpt, hpt, sizeof(hpt), hipMemcpyHostToDevice, s));
-    GS_HIP(hipMemcpyAsync(dtab, htab, sizeof(htab), hipMemcpyHostToDevice, s));
+    // stream-ordered copies from host tables the context keeps (they outlive the copies:
+    // nothing below waits for the stream)
+    c->reg_split_hpt.assign(hpt, hpt + sizeof(hpt) / sizeof(hpt[0]));
+    c->reg_split_htab.assign(&htab[0][0], &htab[0][0] + sizeof(htab) / sizeof(int64_t));
+    GS_HIP(hipMemcpyAsync(dpt, c->reg_split_hpt.data(), sizeof(hpt), hipMemcpyHostToDevice, s));
+    GS_HIP(hipMemcpyAsync(dtab, c->reg_split_htab.data(), sizeof(htab), hipMemcpyHostToDevice, s));
     auto *ells = (uint4 *)c->buf("er_reg_split_ell").ensure(sizeof(uint4) * n);
     double *ellvs = ufast ? nullptr : (double *)c->buf("er_reg_split_ellv").ensure(sizeof(double) * 8 * n);
     auto *ocols = (uint16_t *)c->buf("er_reg_split_ocol").ensure(sizeof(uint16_t) * (nov + 1));
@@ -398,28 +403,49 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     if (Gs == 4) regwide_split_launch_g4(B, Rs, ufast, dyns, grid, s);
     else regwide_split_launch_g8(B, Rs, ufast, dyns, grid, s);
     GS_HIP(hipGetLastError());
-    int32_t aborted = 0;
-    GS_HIP(hipMemcpyAsync(&aborted, B.abortf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    GS_HIP(hipStreamSynchronize(s));
-    if (aborted) {
-        // the parts of a column could not all be resident at once (another process or
-        // stream held CUs): solve the tail columns again, whole, one workgroup each, and
-        // keep the split form off for this context from now on
+    // If the parts of a column could not all be resident at once (another process or
+    // stream held CUs), the hand-offs gave up and set the abort word: the tail columns
+    // are then solved again, whole, one workgroup each -- by a launch gated on that
+    // word on the device (it exits at once when the split form completed), so no host
+    // round trip.  The host reads the word later, without waiting (split_abort_poll),
+    // counts the abort and keeps the split form off for this graph.
+    RegArgs Cw = A;
+    Cw.col0 = col0 + W;
+    Cw.ncols = tailn;
+    Cw.Xc = Xc + W * ldn;
+    Cw.prof = nullptr;
+    Cw.gate = B.abortf;
+    const int64_t ts = std::min<int64_t>(tailn, wslots > 1 ? wslots : slots);
+    if (G == 1) regwide_launch_g1(Cw, rsel, ufast, dyn, (unsigned)ts, s);
+    else if (G == 2) regwide_launch_g2(Cw, rsel, ufast, dyn, (unsigned)ts, s);
+    else if (G == 4) regwide_launch_g4(Cw, rsel, ufast, dyn, (unsigned)ts, s);
+    else regwide_launch_g8(Cw, rsel, ufast, dyn, (unsigned)ts, s);
+    GS_HIP(hipGetLastError());
+    if (!c->split_abort_host) {
+        GS_HIP(hipHostMalloc((void **)&c->split_abort_host, sizeof(int32_t), hipHostMallocDefault));
+        GS_HIP(hipEventCreateWithFlags(&c->split_abort_ev, hipEventDisableTiming));
+    }
+    *c->split_abort_host = 0;
+    GS_HIP(hipMemcpyAsync(c->split_abort_host, B.abortf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    GS_HIP(hipEventRecord(c->split_abort_ev, s));
+    c->split_abort_pending = true;
+    c->split_abort_parts = P;
+}
+
+// The abort word of the last split launch, once its copy has landed (never waits unless
+// `wait`): an abort turns the split form off for the graph it happened on.
+void split_abort_poll(gs_ctx *c, bool wait) {
+    if (!c->split_abort_pending) return;
+    if (!wait && hipEventQuery(c->split_abort_ev) != hipSuccess) return;
+    if (wait) GS_HIP(hipEventSynchronize(c->split_abort_ev));
+    c->split_abort_pending = false;
+    if (*c->split_abort_host) {
         c->reg_split_off = true;
+        c->reg_split_off_epoch = c->g.epoch;
+        c->split_aborts += 1;
         prof_note(c, "cg_split_abort");
         fprintf(stderr, "[gsparse] split CG hand-off timed out (%d parts); tail re-solved whole, "
-                        "split form off for this context\n", P);
-        RegArgs Cw = A;
-        Cw.col0 = col0 + W;
-        Cw.ncols = tailn;
-        Cw.Xc = Xc + W * ldn;
-        Cw.prof = nullptr;
-        const int64_t ts = std::min<int64_t>(tailn, wslots > 1 ? wslots : slots);
-        if (G == 1) regwide_launch_g1(Cw, rsel, ufast, dyn, (unsigned)ts, s);
-        else if (G == 2) regwide_launch_g2(Cw, rsel, ufast, dyn, (unsigned)ts, s);
-        else if (G == 4) regwide_launch_g4(Cw, rsel, ufast, dyn, (unsigned)ts, s);
-        else regwide_launch_g8(Cw, rsel, ufast, dyn, (unsigned)ts, s);
-        GS_HIP(hipGetLastError());
+                        "split form off for this graph\n", c->split_abort_parts);
     }
 }
 

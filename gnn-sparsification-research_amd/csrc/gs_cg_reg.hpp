@@ -83,6 +83,9 @@ struct RegArgs {
     int32_t *abortf;      // set when a hand-off poll gave up
     int32_t spinmax;      // wait budget of one hand-off poll, in ticks of the 100 MHz
                           // constant clock (wall_clock64); 0: give up at once
+    const int32_t *gate;  // optional: solve the columns only if *gate != 0 (the whole-column
+                          // re-solve of a split tail whose hand-offs gave up; read once at
+                          // launch, wave-uniform), else every column as usual
 };
 static constexpr int kRegPartTab = 4 * kRegMaxChunks + 4;
 
@@ -373,7 +376,8 @@ __global__ void __launch_bounds__(NT) k_cg_regres(RegArgs A) {
         tmark = tn;
     };
 
-    for (int64_t ci = blockIdx.x; ci < A.ncols; ci += gridDim.x) {
+    const int64_t ncols = (A.gate && *A.gate == 0) ? 0 : A.ncols;
+    for (int64_t ci = blockIdx.x; ci < ncols; ci += gridDim.x) {
         const int64_t c = A.col0 + ci;
         AgD r[R], x[R];
         // r = b.copy(); rho_0 = b.b

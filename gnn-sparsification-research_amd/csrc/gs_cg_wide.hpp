@@ -411,7 +411,8 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         tmark = tn;
     };
 
-    for (int64_t ci = group; ci < A.ncols; ci += ngroups) {
+    const int64_t ncols = (A.gate && *A.gate == 0) ? 0 : A.ncols;
+    for (int64_t ci = group; ci < ncols; ci += ngroups) {
         const int64_t c = A.col0 + ci;
         double r[R], x[QR ? 1 : R], qr[QR ? R : 1];
         // QR: x of the slots in this column's Xc rows (raw buffer; rows past n dropped)

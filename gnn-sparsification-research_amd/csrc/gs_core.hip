@@ -32,7 +32,7 @@ void prof_end(gs_ctx *c, hipEvent_t start, const char *name, double bytes) {
     GS_HIP(hipEventCreate(&e));
     GS_HIP(hipEventRecord(e, c->stream));
     c->pending.push_back(ProfPending{name, start, e, bytes});
-    if (c->pending.size() > 4096) prof_flush(c);
+    if (c->pending.size() >= (size_t)kProfPendingMax) prof_flush(c);
 }
 
 void prof_note(gs_ctx *c, const char *name) {
@@ -46,8 +46,18 @@ void prof_note(gs_ctx *c, const char *name) {
 }
 
 void prof_flush(gs_ctx *c) {
+    split_abort_poll(c, true);
     if (c->pending.empty()) return;
     GS_HIP(hipStreamSynchronize(c->stream));
+    bool slots = false;
+    for (auto &p : c->pending) slots = slots || p.its_slot >= 0;
+    if (slots) {
+        std::vector<int64_t> its(c->pending.size(), 0);
+        GS_HIP(hipMemcpy(its.data(), c->buf("prof_its").as<int64_t>(), sizeof(int64_t) * its.size(),
+                         hipMemcpyDeviceToHost));
+        for (auto &p : c->pending)
+            if (p.its_slot >= 0) p.bytes += p.its_bytes * (double)its[(size_t)p.its_slot];
+    }
     for (auto &p : c->pending) {
         float ms = 0.f;
         GS_HIP(hipEventElapsedTime(&ms, p.start, p.stop));
@@ -198,6 +208,8 @@ void gs_destroy(gs_ctx *c) {
     for (auto &e : c->aux_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
+    if (c->split_abort_ev) (void)hipEventDestroy(c->split_abort_ev);
+    if (c->split_abort_host) (void)hipHostFree(c->split_abort_host);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -238,6 +250,7 @@ int gs_synchronize(gs_ctx *c) {
     return guard([&] {
         GS_CHECK(c, GS_EINVAL, "null context");
         GS_HIP(hipStreamSynchronize(c->stream));
+        split_abort_poll(c, true);
     });
 }
 

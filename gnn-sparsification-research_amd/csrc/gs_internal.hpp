@@ -72,7 +72,13 @@ struct ProfPending {
     std::string name;
     hipEvent_t start, stop;
     double bytes;
+    // optional: + its_bytes x (an int64 the device wrote to slot its_slot of the
+    // context's "prof_its" buffer), read when the entries are flushed -- e.g. the CG's
+    // bytes per executed iteration, without a host round trip per solve
+    int64_t its_slot = -1;
+    double its_bytes = 0.0;
 };
+static constexpr int kProfPendingMax = 4096;
 
 struct Graph {
     int64_t n = 0, nnz = 0;
@@ -117,8 +123,23 @@ struct ErState {
     DevBuf rawbuf;    // staging for host-streamed raw normals
     int pcur = 0;     // which of P0/P1 holds the current p
     bool solved = false;
+    int64_t proj_c0 = 0, proj_c1 = 0;  // JL columns of Y the projection fills (a rank's slice)
+    std::vector<int64_t> prep_key;      // (graph epoch, k, reg) the state above was built for
+    void *rr_zeroed = nullptr;          // Rr allocation whose row padding has been zeroed
+    // mode 4 / 5 setup read back once per (graph epoch, reg): unit-weight flags, SELL
+    // entry count and slice widths (no host round trip on later solves)
+    std::vector<int64_t> unit_key;
+    int32_t unit_flags = 0;
+    int64_t sell_sent = 0;
+    std::vector<int32_t> sell_wid;
 };
 
+}  // namespace gs
+
+struct gs_ctx;
+namespace gs {
+void project_rows(gs_ctx *c, int64_t e0, int64_t e1, const double *draw, int64_t kraw, int64_t col0,
+                  int64_t col1, double sqrt_k);
 }  // namespace gs
 
 struct gs_ctx {
@@ -135,6 +156,8 @@ struct gs_ctx {
     std::vector<gs::ProfPending> pending;
     gs::Graph g;
     gs::ErState er;
+    std::vector<uint64_t> zig_key;  // (PCG64 state, stream length, block) of a parsed stream
+    int64_t zig_draws = 0;          // draws known to cover it
     gs::DevBuf scratch[6];
     gs::DevBuf outbuf, inbuf, inbuf2;
     std::map<std::string, gs::DevBuf> named;  // per-subsystem buffers (backbone, ...)
@@ -148,6 +171,14 @@ struct gs_ctx {
     int64_t reg_nov = 0;
     std::vector<int64_t> reg_hch;  // host copy of the chunk table (outlives its async copy)
     bool reg_split_off = false;
+    int64_t reg_split_off_epoch = -1;      // graph epoch the split form was turned off for
+    std::vector<int32_t> reg_split_hpt;    // host copies of the split tables (outlive their
+    std::vector<int64_t> reg_split_htab;   // stream-ordered uploads)
+    int32_t *split_abort_host = nullptr;   // pinned: the last split launch's abort word
+    hipEvent_t split_abort_ev = nullptr;   // its copy has landed
+    bool split_abort_pending = false;
+    int split_abort_parts = 0;
+    int64_t split_aborts = 0;              // aborts seen by this context
     gs::DevBuf &buf(const char *name) { return named[name]; }
 };
 
@@ -203,6 +234,7 @@ void ensure_transpose(gs_ctx *c);
 // of L_reg (CSR lp/li/lv) into Xc (column-major, ldn per column)
 bool cg_regres_applies(int64_t n, int T, const int64_t *len);
 bool cg_regres_wide(int64_t n, int T, const int64_t *len);  // its 512-thread form applies
+void split_abort_poll(gs_ctx *c, bool wait);
 void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li, const double *lv,
                      int unit, int dcount, const double *diag, const double *Rr, int64_t ld,
                      int64_t col0, int64_t ncols, int32_t maxiter, double rtol, int T,

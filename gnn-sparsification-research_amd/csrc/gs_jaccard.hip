@@ -197,11 +197,12 @@ __global__ void k_jac_owner_list(const int64_t *__restrict__ ip, const int32_t *
 
 // cut rows: R[r] = first row u with S[u] >= total * r / P (S: exclusive prefix of the
 // row work, S[n] = total), R[0] = 0, R[P] = n; then E[r] = ip[R[r]] and
-// O[r] = opre[E[r]].  One thread per cut.  out = [R | E | O], 3 (P + 1) values.
+// O[r] = opre[E[r]].  One thread per cut (P + 1 of them, any P: the grid covers
+// them all).  out = [R | E | O], 3 (P + 1) values.
 __global__ void k_jac_cuts(const int64_t *__restrict__ S, const int64_t *__restrict__ ip,
                            const int64_t *__restrict__ opre, int64_t n, int P,
                            int64_t *__restrict__ out) {
-    const int r = threadIdx.x;
+    const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (r > P) return;
     const int64_t total = S[n];
     int64_t R;
@@ -568,7 +569,7 @@ const JacShares &jaccard_shares(gs_ctx *c, int P) {
     if (n) k_jac_rowwork<<<grid_for(n, 4, 4096), 256, 0, st>>>(ip, ix, n, work);
     exclusive_scan_i64(c, work, S, n + 1);
     auto *dcut = (int64_t *)c->buf("jac_cutbuf").ensure(sizeof(int64_t) * 3 * (P + 1));
-    k_jac_cuts<<<1, 128, 0, st>>>(S, ip, opre, n, P, dcut);
+    k_jac_cuts<<<(unsigned)((P + 1 + 127) / 128), 128, 0, st>>>(S, ip, opre, n, P, dcut);
     GS_HIP(hipGetLastError());
     JacShares sh;
     sh.cuts.resize(3 * (P + 1));

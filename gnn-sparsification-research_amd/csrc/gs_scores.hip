@@ -259,8 +259,8 @@ int gs_jaccard(gs_ctx *c, int64_t e0, int64_t e1, double *out, int loc) {
 int gs_jaccard_part(gs_ctx *c, int part, int nparts, double *out, int loc) {
     return guard([&] {
         GS_CHECK(c, GS_EINVAL, "null context");
-        GS_CHECK(nparts >= 1 && 0 <= part && part < nparts, GS_EINVAL, "bad part %d of %d", part,
-                 nparts);
+        GS_CHECK(nparts >= 1 && nparts <= 4096 && 0 <= part && part < nparts, GS_EINVAL,
+                 "bad part %d of %d (at most 4096 parts)", part, nparts);
         GS_HIP(hipSetDevice(c->device));
         Graph &g = c->g;
         const int64_t nnz = g.nnz;

@@ -58,9 +58,12 @@ SIGNATURES = {
     "gs_er_prepare": (_int, [_vp, _i64, _f64, ctypes.POINTER(_i64)]),
     "gs_er_project_rows": (_int, [_vp, _i64, _i64, _vp, _int, _f64]),
     "gs_er_project_pcg64": (_int, [_vp, _u64, _u64, _u64, _u64, _f64]),
+    "gs_er_project_pcg64_cols": (_int, [_vp, _u64, _u64, _u64, _u64, _f64, _i64, _i64]),
+    "gs_er_project_rows_cols": (_int, [_vp, _i64, _i64, _vp, _int, _f64, _i64, _i64]),
     "gs_er_solve": (_int, [_vp, _i64, _i64, _i32, _f64, _i32]),
     "gs_er_scores": (_int, [_vp, _i64, _i64, _i64, _i64, _int, _vp, _int]),
     "gs_er_iterations": (_int, [_vp, _vp, _int]),
+    "gs_er_copy_z": (_int, [_vp, _i64, _i64, _vp, _int]),
     "gs_er_split": (_int, [_i64, _i32, _vp]),
     "gs_topk_mask": (_int, [_vp, _vp, _int, _i64, _i64, _i64, _int, _vp, _int,
                             ctypes.POINTER(_f64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),

@@ -15,6 +15,9 @@ SURVEY §8(e):
     edge ranges (equal counts, or equal per-edge work d_u + d_v for skewed
     graphs), then an all-gather of the fp64 scores so every rank can run the
     global top-k.
+  * the global top-k (sharded_sparsify): every rank holds the all-gathered
+    scores and runs the same radix select on its own device -- the kept set is
+    identical on every rank and to one GPU's, with no further exchange.
   * ApproxER: the k JL columns are independent CG solves.  Rank blocks are
     nodes of NumPy's pairwise-sum tree over k (gs_er_split), so each rank's
     per-edge partial sum is exactly a subtree of the reference's
@@ -169,6 +172,44 @@ def sharded_edge_scores(engine, comm: Comm, metric: str, bounds: list[int] | Non
     return comm.all_gather_padded(comm.tensor(local), sizes)
 
 
+def sharded_sparsify(engine, comm: Comm, scores, num_edges: int, retention_ratio: float,
+                     keep_lowest: bool = False, tie_break: str = "stable", out=None):
+    """GraphSparsifier.sparsify's top-k (core.py:221-242) after the score
+    all-gather: every rank holds the same full score vector (sharded_*), so every
+    rank selects the same global top ``int(E*r)`` -- the radix select of
+    gs_topk_mask on its own device, no further exchange.
+
+    tie_break "stable": the device tie rule (= np.argsort(kind='stable'));
+    "numpy": an ambiguous tie block at the cut is resolved by the reference's own
+    np.argsort call on the host (small graphs; identical on every rank of a node).
+    Returns (mask, info): a bool tensor on the comm device (a CPU tensor for gloo)
+    and the cut / #beyond / #tied of the selection."""
+    if not 0 < retention_ratio <= 1:
+        raise ValueError(f"retention_ratio must be in (0, 1], got {retention_ratio}")
+    cuda = comm.device.type == "cuda"
+    if retention_ratio == 1.0:
+        m = torch.ones(num_edges, dtype=torch.bool, device=comm.device if cuda else "cpu")
+        return m, {"cut": None, "beyond": num_edges, "tied": 0, "need": 0, "ambiguous": False}
+    num_keep = int(num_edges * retention_ratio)
+    if cuda:
+        if out is None:
+            out = torch.empty(num_edges, dtype=torch.uint8, device=comm.device)
+        mask, cut, nb, nt = engine.topk_mask(scores, num_edges, num_keep, keep_lowest, out=out)
+    else:
+        s = scores.numpy() if isinstance(scores, torch.Tensor) else np.asarray(scores)
+        m, cut, nb, nt = engine.topk_mask(s, num_edges, num_keep, keep_lowest)
+        mask = torch.from_numpy(np.ascontiguousarray(m))
+    need = num_keep - nb
+    info = {"cut": cut, "beyond": nb, "tied": nt, "need": need, "ambiguous": 0 < need < nt}
+    if info["ambiguous"] and tie_break == "numpy":
+        from .selection import numpy_topk_mask
+
+        s = scores.cpu().numpy() if isinstance(scores, torch.Tensor) else np.asarray(scores)
+        m = torch.from_numpy(numpy_topk_mask(s, num_edges, num_keep, keep_lowest))
+        mask = m.to(comm.device) if cuda else m
+    return mask.view(torch.bool) if mask.dtype == torch.uint8 else mask, info
+
+
 def sharded_backbone(comm: Comm, edge_index: np.ndarray, num_nodes: int,
                      edge_weights: np.ndarray, epsilon: float = 1e-9, mask_fn=None) -> np.ndarray:
     """metric_backbone keep mask with the per-source searches split over ranks
@@ -243,13 +284,16 @@ def sharded_approx_er(engine, comm: Comm, epsilon: float = 0.3, seed: int = 42,
     if m == 0:
         return comm.tensor(np.zeros(engine.nnz))
     depth, bounds, runs = er_rank_blocks(k, comm.world)
+    a, b = runs[comm.rank]
+    # this rank's JL columns only: the whole normal stream is parsed (it is sequential),
+    # but only R[:, c0:c1] is stored and projected (metrics.py:272-275)
+    cols = (bounds[a], bounds[b]) if b > a else (0, min(k, 1))
     if rng_mode == "device":
-        engine.er_project_device(rng, k)
+        engine.er_project_device(rng, k, cols=cols)
     else:
-        engine.er_project_host(rng, k)
+        engine.er_project_host(rng, k, cols=cols)
     covers = [dyadic_cover(a, b) for a, b in runs]
     slots = max(1, max(len(cv) for cv in covers))
-    a, b = runs[comm.rank]
     cuda = comm.device.type == "cuda"
     local = torch.zeros((slots, engine.nnz), dtype=torch.float64,
                         device=comm.device if cuda else "cpu")

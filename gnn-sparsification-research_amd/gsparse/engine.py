@@ -185,10 +185,12 @@ class Engine:
         self.m = m.value
         return self.m
 
-    def er_project_host(self, rng: np.random.Generator, k: int):
+    def er_project_host(self, rng: np.random.Generator, k: int, cols=None):
         """Stream R = rng.standard_normal((m, k)) row-chunk by row-chunk (identical
         NumPy stream, verified chunk-invariant) into Y = B @ (R / sqrt(k)),
-        generating chunk i+1 on a worker thread while chunk i is projected."""
+        generating chunk i+1 on a worker thread while chunk i is projected.
+        cols = (c0, c1): form only Y[:, c0:c1] (a rank's JL columns)."""
+        c0, c1 = cols if cols is not None else (0, k)
         m = self.m
         sqrt_k = float(np.sqrt(k))
         rows = max(1, _ROW_CHUNK_BYTES // (8 * k))
@@ -207,10 +209,13 @@ class Engine:
             if item is None:
                 break
             e0, e1, raw = item
-            self.ctx.call("gs_er_project_rows", e0, e1, ptr(raw), GS_HOST, sqrt_k)
+            self.ctx.call("gs_er_project_rows_cols", e0, e1, ptr(raw), GS_HOST, sqrt_k, c0, c1)
         th.join()
 
-    def er_project_device(self, rng: np.random.Generator, k: int):
+    def er_project_device(self, rng: np.random.Generator, k: int, cols=None):
+        """The same R drawn on the device (PCG64 + NumPy's ziggurat); cols = (c0, c1):
+        every normal is parsed, only R[:, c0:c1] is stored and projected."""
+        c0, c1 = cols if cols is not None else (0, k)
         st = rng.bit_generator.state
         if st.get("bit_generator") != "PCG64":
             raise NotImplementedError("device ziggurat supports the PCG64 bit generator")
@@ -218,8 +223,8 @@ class Engine:
         m64 = (1 << 64) - 1
         if st.get("has_uint32"):
             raise NotImplementedError("PCG64 state with a buffered uint32")
-        self.ctx.call("gs_er_project_pcg64", s >> 64, s & m64, inc >> 64, inc & m64,
-                      float(np.sqrt(k)))
+        self.ctx.call("gs_er_project_pcg64_cols", s >> 64, s & m64, inc >> 64, inc & m64,
+                      float(np.sqrt(k)), c0, c1)
 
     def er_solve(self, col0: int, col1: int, maxiter: int, rtol: float, blas_threads: int):
         self.ctx.call("gs_er_solve", col0, col1, maxiter, rtol, blas_threads)
@@ -235,6 +240,12 @@ class Engine:
         it = np.empty(self.k, dtype=np.int32)
         self.ctx.call("gs_er_iterations", ptr(it), GS_HOST)
         return it
+
+    def er_z(self, col0: int, col1: int) -> np.ndarray:
+        """The solved Z columns [col0, col1) as an (n, col1 - col0) array (gs_er_copy_z)."""
+        z = np.empty((self.n, col1 - col0), dtype=np.float64)
+        self.ctx.call("gs_er_copy_z", col0, col1, ptr(z), GS_HOST)
+        return z
 
     def approx_er(self, epsilon: float = 0.3, seed: int = 42, max_cg_iters: int = 500,
                   cg_tol: float = 1e-6, blas_threads: int | None = None,
@@ -305,15 +316,27 @@ class Engine:
                       GS_HOST, int(src.shape[0]), int(num_nodes), ptr(pick), GS_HOST)
         return pick[:num_nodes]
 
-    def topk_mask(self, scores, num_edges: int, num_keep: int, keep_lowest: bool):
-        """Device mask + (cut, #beyond, #tied) -- see gs_topk_mask."""
-        scores = np.ascontiguousarray(scores, dtype=np.float64) if isinstance(scores, np.ndarray) \
-            else scores
-        sloc = GS_HOST if isinstance(scores, np.ndarray) else GS_DEVICE
+    def topk_mask(self, scores, num_edges: int, num_keep: int, keep_lowest: bool, out=None):
+        """Device mask + (cut, #beyond, #tied) -- see gs_topk_mask.  ``scores``: a
+        numpy array or a CUDA float64 tensor; ``out``: an optional CUDA uint8/bool
+        tensor of >= num_edges elements that receives the mask on the device (then
+        returned as is) instead of a host numpy bool array."""
+        if isinstance(scores, np.ndarray):
+            scores = np.ascontiguousarray(scores, dtype=np.float64)
+            sloc = GS_HOST
+        else:
+            sloc = GS_DEVICE if scores.is_cuda else GS_HOST
+            if sloc == GS_HOST:
+                scores = np.ascontiguousarray(scores.numpy(), dtype=np.float64)
         nnz = int(scores.shape[0])
-        mask = np.zeros(num_edges, dtype=np.uint8)
+        if out is None:
+            mask, mloc = np.zeros(num_edges, dtype=np.uint8), GS_HOST
+        else:
+            if not out.is_cuda or out.numel() < num_edges or out.element_size() != 1:
+                raise ValueError("out must be a CUDA uint8/bool tensor of >= num_edges elements")
+            mask, mloc = out, GS_DEVICE
         cut, nb, nt = ctypes.c_double(0), ctypes.c_int64(0), ctypes.c_int64(0)
         self.ctx.call("gs_topk_mask", ptr(scores), sloc, nnz, num_edges, num_keep,
-                      int(keep_lowest), ptr(mask), GS_HOST, ctypes.byref(cut), ctypes.byref(nb),
+                      int(keep_lowest), ptr(mask), mloc, ctypes.byref(cut), ctypes.byref(nb),
                       ctypes.byref(nt))
-        return mask.view(bool), cut.value, nb.value, nt.value
+        return (mask.view(bool) if out is None else out), cut.value, nb.value, nt.value

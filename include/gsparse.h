@@ -151,17 +151,27 @@ int gs_feature_cosine_f64(gs_ctx *ctx, const double *x, int64_t f, int x_loc, in
  *   NumPy pairwise order (:292-293).  [col0,col1) must be a node of the
  *   pairwise tree of k (the whole range, or a gs_er_split() block); when
  *   finalize != 0 the clamp of :296-297 is applied.
- * gs_er_iterations: CG iterations each column ran (k values). */
+ * gs_er_iterations: CG iterations each column ran (k values).
+ * gs_er_copy_z: the solved Z columns [col0, col1) (metrics.py:285-289's
+ *   Z[:, i] = cg(...)), n rows x (col1 - col0) row-major -- a parity read-out. */
 int gs_er_prepare(gs_ctx *ctx, int64_t k, double reg, int64_t *m_out);
 int gs_er_project_rows(gs_ctx *ctx, int64_t e0, int64_t e1, const double *raw, int loc,
                        double sqrt_k);
 int gs_er_project_pcg64(gs_ctx *ctx, uint64_t state_hi, uint64_t state_lo, uint64_t inc_hi,
                         uint64_t inc_lo, double sqrt_k);
+/* Column-slice forms (a rank's JL columns): the normal stream /
+ * the host rows are the same whole NumPy stream, but only Y[:, col0:col1] is
+ * formed; gs_er_solve then accepts column ranges inside [col0, col1). */
+int gs_er_project_pcg64_cols(gs_ctx *ctx, uint64_t state_hi, uint64_t state_lo, uint64_t inc_hi,
+                             uint64_t inc_lo, double sqrt_k, int64_t col0, int64_t col1);
+int gs_er_project_rows_cols(gs_ctx *ctx, int64_t e0, int64_t e1, const double *raw, int loc,
+                            double sqrt_k, int64_t col0, int64_t col1);
 int gs_er_solve(gs_ctx *ctx, int64_t col0, int64_t col1, int32_t maxiter, double rtol,
                 int32_t blas_threads);
 int gs_er_scores(gs_ctx *ctx, int64_t col0, int64_t col1, int64_t e0, int64_t e1,
                  int finalize, double *out, int loc);
 int gs_er_iterations(gs_ctx *ctx, int32_t *iters, int loc);
+int gs_er_copy_z(gs_ctx *ctx, int64_t col0, int64_t col1, double *out, int loc);
 /* Column blocks of the pairwise tree of k at depth log2(parts): bounds has
  * parts+1 entries.  parts must be a power of two. */
 int gs_er_split(int64_t k, int32_t parts, int64_t *bounds);

@@ -49,6 +49,7 @@ def lib():
         L.oracle_pairwise_sum_f64.restype = ctypes.c_double
         L.oracle_pairwise_sum_f32.restype = ctypes.c_float
         L.oracle_metric_backbone.restype = ctypes.c_int64
+        L.oracle_metric_backbone_rows.restype = ctypes.c_int64
         L.oracle_ddot.restype = ctypes.c_double
         _LIB = L
     return _LIB
@@ -385,8 +386,9 @@ def scores_to_cost(scores, metric_key):
     return 1.0 / proximity - 1.0
 
 
-def metric_backbone(edge_index, n, w, epsilon=1e-9, return_relax=False):
-    """metric_backbone.py:59-111 restated as bounded per-row Dijkstra (oracle.c)."""
+def _backbone_graph(edge_index, n, w):
+    """G of metric_backbone.py:70-79 (u<v columns, min weight over duplicates) as a
+    symmetric CSR, plus the columns grouped by row."""
     ei = np.asarray(edge_index, dtype=np.int64)
     rows, cols = np.ascontiguousarray(ei[0]), np.ascontiguousarray(ei[1])
     E = len(rows)
@@ -415,6 +417,13 @@ def metric_backbone(edge_index, n, w, epsilon=1e-9, return_relax=False):
     corder = np.argsort(rows, kind="stable").astype(np.int64)
     optr = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(np.bincount(rows, minlength=n), out=optr[1:])
+    return rows, cols, w, gp, gi, gw_, corder, optr
+
+
+def metric_backbone(edge_index, n, w, epsilon=1e-9, return_relax=False):
+    """metric_backbone.py:59-111 restated as bounded per-row Dijkstra (oracle.c)."""
+    rows, cols, w, gp, gi, gw_, corder, optr = _backbone_graph(edge_index, n, w)
+    E = len(rows)
     keep = np.zeros(E, dtype=np.uint8)
     relax = ctypes.c_int64(0)
     lib().oracle_metric_backbone(ctypes.c_int64(n), _p(gp, _i64p), _p(gi, _i32p), _p(gw_, _f64p),
@@ -423,6 +432,36 @@ def metric_backbone(edge_index, n, w, epsilon=1e-9, return_relax=False):
                                  _p(keep, _u8p), ctypes.byref(relax))
     keep = keep.astype(bool)
     return (keep, relax.value) if return_relax else keep
+
+
+def metric_backbone_rows(edge_index, n, w, sources, epsilon=1e-9, threads=None):
+    """metric_backbone.py:86-111 for the columns whose row is in ``sources`` only:
+    one bounded Dijkstra per listed row (oracle.c), the rows spread over host
+    threads (ctypes drops the GIL).  Returns (keep bool[E], decided bool[E])."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    rows, cols, w, gp, gi, gw_, corder, optr = _backbone_graph(edge_index, n, w)
+    E = len(rows)
+    src = np.unique(np.asarray(sources, dtype=np.int64))
+    threads = threads or min(16, os.cpu_count() or 1, max(1, len(src)))
+    keep = np.zeros(E, dtype=np.uint8)
+
+    def run(sel):
+        sel = np.ascontiguousarray(sel, dtype=np.int64)
+        k = np.zeros(E, dtype=np.uint8)  # one output per thread: rows never share a column
+        lib().oracle_metric_backbone_rows(ctypes.c_int64(n), _p(gp, _i64p), _p(gi, _i32p),
+                                          _p(gw_, _f64p), _p(cols, _i64p), _p(w, _f64p),
+                                          ctypes.c_double(epsilon), _p(corder, _i64p),
+                                          _p(optr, _i64p), ctypes.c_int64(len(sel)),
+                                          _p(sel, _i64p), _p(k, _u8p), None)
+        return sel, k
+
+    with ThreadPoolExecutor(threads) as ex:
+        for sel, k in ex.map(run, [src[i::threads] for i in range(threads)]):
+            dec = np.isin(rows, sel)
+            keep[dec] = k[dec]
+    decided = np.isin(rows, src)
+    return keep.astype(bool), decided
 
 
 def sampled_mask(scores, num_edges, retention_ratio, seed=42):

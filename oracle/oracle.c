@@ -353,10 +353,12 @@ static hent heap_pop(hent *h, int64_t *hn) {
 /* gp/gi/gw: symmetric CSR of G (built by the caller from the u<v columns,
  * min weight over duplicates).  rows/cols/w: the E edge_index columns.
  * order/optr: columns grouped by row (order = column ids sorted by row). */
-int64_t oracle_metric_backbone(int64_t n, const int64_t *gp, const int32_t *gi, const double *gw,
-                               int64_t E, const int64_t *rows, const int64_t *cols,
-                               const double *w, double eps, const int64_t *order,
-                               const int64_t *optr, uint8_t *keep, int64_t *relax_out) {
+/* sel/nsel: the source rows to decide (sel == NULL: every row 0..n-1); the
+ * columns of other rows are left untouched in keep */
+static int64_t backbone_rows(int64_t n, const int64_t *gp, const int32_t *gi, const double *gw,
+                             const int64_t *cols, const double *w, double eps,
+                             const int64_t *order, const int64_t *optr, const int64_t *sel,
+                             int64_t nsel, uint8_t *keep, int64_t *relax_out) {
     double *dist = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
     uint8_t *done = (uint8_t *)calloc((size_t)(n > 0 ? n : 1), 1);
     uint8_t *tgt = (uint8_t *)calloc((size_t)(n > 0 ? n : 1), 1);
@@ -365,8 +367,9 @@ int64_t oracle_metric_backbone(int64_t n, const int64_t *gp, const int32_t *gi, 
     int32_t *touched = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
     int64_t relax = 0;
     for (int64_t i = 0; i < n; ++i) dist[i] = INFINITY;
-    for (int64_t u = 0; u < n; ++u) {
-        if (optr[u] == optr[u + 1]) continue;
+    for (int64_t si = 0; si < (sel ? nsel : n); ++si) {
+        const int64_t u = sel ? sel[si] : si;
+        if (u < 0 || u >= n || optr[u] == optr[u + 1]) continue;
         double wmax = -INFINITY;
         int64_t ntg = 0;
         for (int64_t j = optr[u]; j < optr[u + 1]; ++j) {
@@ -410,4 +413,22 @@ int64_t oracle_metric_backbone(int64_t n, const int64_t *gp, const int32_t *gi, 
     if (relax_out) *relax_out = relax;
     free(dist); free(done); free(tgt); free(h); free(touched);
     return 0;
+}
+
+int64_t oracle_metric_backbone(int64_t n, const int64_t *gp, const int32_t *gi, const double *gw,
+                               int64_t E, const int64_t *rows, const int64_t *cols,
+                               const double *w, double eps, const int64_t *order,
+                               const int64_t *optr, uint8_t *keep, int64_t *relax_out) {
+    (void)E; (void)rows;
+    return backbone_rows(n, gp, gi, gw, cols, w, eps, order, optr, NULL, 0, keep, relax_out);
+}
+
+/* The same decisions for the columns of the listed source rows only (the
+ * sampled-row pin of large graphs: one bounded Dijkstra per listed row). */
+int64_t oracle_metric_backbone_rows(int64_t n, const int64_t *gp, const int32_t *gi,
+                                    const double *gw, const int64_t *cols, const double *w,
+                                    double eps, const int64_t *order, const int64_t *optr,
+                                    int64_t nsel, const int64_t *sel, uint8_t *keep,
+                                    int64_t *relax_out) {
+    return backbone_rows(n, gp, gi, gw, cols, w, eps, order, optr, sel, nsel, keep, relax_out);
 }

@@ -52,14 +52,32 @@ class OracleEngine:
     def adamic_adar(self, e0=0, e1=None, out=None):
         return O.adamic_adar(self.ip, self.ix)[e0:e1]
 
+    def topk_mask(self, scores, num_edges, num_keep, keep_lowest, out=None):
+        """gs_topk_mask's contract: the stable-argsort mask + (cut, #beyond, #tied)."""
+        s = np.asarray(scores, dtype=np.float64)
+        mask = np.zeros(num_edges, dtype=bool)
+        if num_keep <= 0:
+            if not keep_lowest:
+                mask[: len(s)] = True
+            return mask, float("nan"), (0 if keep_lowest else len(s)), 0
+        idx = np.argsort(s, kind="stable")
+        sel = idx[:num_keep] if keep_lowest else idx[-num_keep:]
+        mask[sel] = True
+        cut = s[sel[-1]] if keep_lowest else s[sel[0]]
+        beyond = int((s < cut).sum()) if keep_lowest else int((s > cut).sum())
+        return mask, float(cut), beyond, int((s == cut).sum())
+
     def er_prepare(self, k):
         self.k = k
         rows = O.csr_rows(self.ip)
         self.m = int(np.count_nonzero(rows < self.ix))
         return self.m
 
-    def er_project_device(self, rng, k):
-        self.Y, _, _ = O.approx_er_projection(self.ip, self.ix, self.n)
+    def er_project_device(self, rng, k, cols=None):
+        Y, _, _ = O.approx_er_projection(self.ip, self.ix, self.n)
+        c0, c1 = cols if cols is not None else (0, k)
+        self.Y = np.full_like(Y, np.nan)  # columns outside the slice must not be read
+        self.Y[:, c0:c1] = Y[:, c0:c1]
 
     er_project_host = er_project_device
 
@@ -97,6 +115,15 @@ def _worker(rank, world, port, name, q):
         jac_w = sharded_edge_scores(eng, comm, "jaccard",
                                     bounds=work_ranges(g["indptr"], g["indices"], world)).numpy()
         er = sharded_approx_er(eng, comm, blas_threads=1).numpy()
+        from gsparse.distributed import sharded_sparsify
+
+        E = g["edge_index"].shape[1]
+        masks = {}
+        for r in (0.8, 0.5, 0.2):
+            for low in (False, True):
+                for tb in ("numpy", "stable"):
+                    m, _ = sharded_sparsify(eng, comm, torch.from_numpy(jac), E, r, low, tie_break=tb)
+                    masks[(r, low, tb)] = m.numpy().copy()
         bb = None
         if "backbone_jaccard" in g:
             from gsparse.distributed import sharded_backbone
@@ -107,8 +134,12 @@ def _worker(rank, world, port, name, q):
 
             bb = sharded_backbone(comm, g["edge_index"], int(g["num_nodes"]), g["cost_jaccard"],
                                   mask_fn=oracle_part)
+        # every rank selected the same kept set
+        allm = [None] * world
+        dist.all_gather_object(allm, {k: v.tobytes() for k, v in masks.items()})
+        assert all(a == allm[0] for a in allm)
         if rank == 0:
-            q.put((jac, jac_w, er, bb))
+            q.put((jac, jac_w, er, bb, masks))
     finally:
         dist.destroy_process_group()
 
@@ -122,7 +153,7 @@ def test_sharded_equals_single(name, world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, name, q)) for r in range(world)]
     for p in procs:
         p.start()
-    jac, jac_w, er, bb = q.get(timeout=600)
+    jac, jac_w, er, bb, masks = q.get(timeout=600)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -132,6 +163,14 @@ def test_sharded_equals_single(name, world):
     assert np.array_equal(er.view(np.uint64), g["scores_approx_er"].view(np.uint64))
     if bb is not None:
         assert np.array_equal(bb, g["backbone_jaccard"])
+    # the global top-k after the all-gather: the reference's masks (numpy ties) and
+    # np.argsort(kind='stable') (device tie rule), core.py:229-240
+    E = g["edge_index"].shape[1]
+    for (r, low, tb), m in masks.items():
+        if tb == "numpy" and f"mask_jaccard_{r}_{int(low)}" in g:
+            assert np.array_equal(m, g[f"mask_jaccard_{r}_{int(low)}"]), (r, low)
+        if tb == "stable":
+            assert np.array_equal(m, O.topk_mask(g["scores_jaccard"], E, r, low, kind="stable")), (r, low)
 
 
 def test_tree_helpers():

@@ -86,6 +86,29 @@ def test_jaccard_count_shares_vs_oracle(gs, nparts):
         assert bits_equal(out.cpu().numpy(), ref), name
 
 
+@pytest.mark.parametrize("nparts", [127, 128, 200, 1000])
+def test_jaccard_many_count_shares(gs, nparts):
+    """More parts than one 128-thread block of cut threads (every cut
+    must be written): the shares equal the oracle's and the parts' counts rebuild
+    the reference's Jaccard."""
+    for name, ei, n in _graphs():
+        if name == "karate_test":
+            continue
+        ip, ix, _ = O.canonical_csr(ei, n)
+        e = _engine(gs, ei, n)
+        R, Oo = e.jaccard_shares(nparts)
+        Rr, Or = O.jaccard_shares(ip, ix, nparts)
+        assert np.array_equal(R, Rr) and np.array_equal(Oo, Or), name
+        stride = max(1, int(np.diff(Oo).max()))
+        allc = np.zeros(nparts * stride, dtype=np.uint32)
+        for p in range(nparts):
+            c = e.jaccard_part_counts(p, nparts)
+            allc[p * stride: p * stride + len(c)] = c
+        assert bits_equal(e.jaccard_from_counts(nparts, allc, stride), O.jaccard(ip, ix)), name
+    with pytest.raises(ValueError):
+        e.jaccard_part(0, 5000)
+
+
 def test_jaccard_count_shares_errors(gs):
     g = load_golden("karate_test")
     e = _engine(gs, g["edge_index"], int(g["num_nodes"]))
