@@ -52,7 +52,7 @@ __global__ void k_ell8_fill(int32_t r0, int32_t n, int T, const int64_t *__restr
                             const int32_t *__restrict__ li, const double *__restrict__ lv,
                             const int64_t *__restrict__ optr, uint4 *__restrict__ ell,
                             double *__restrict__ ellv, uint16_t *__restrict__ ocol,
-                            double *__restrict__ oval) {
+                            double *__restrict__ oval, uint8_t *__restrict__ rflag) {
     for (int64_t i = r0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e0 = lp[i], len = lp[i + 1] - e0;
@@ -61,12 +61,15 @@ __global__ void k_ell8_fill(int32_t r0, int32_t n, int T, const int64_t *__restr
             return (dslot0 >= 0 && li[e] == i) ? dcode : p_code(li[e], T, tab);
         };
         uint32_t w[4] = {0, 0, 0, 0};
+        bool glob = false;
         for (int k = 0; k < 8; ++k) {
             const uint32_t cc = k < len ? code(e0 + k) : pad;
+            glob = glob || (cc & 0x8000u) != 0;
             w[k >> 1] |= cc << (16 * (k & 1));
             if (ellv) ellv[i * 8 + k] = k < len ? lv[e0 + k] : 0.0;
         }
         ell[i] = make_uint4(w[0], w[1], w[2], w[3]);
+        if (rflag) rflag[i] = (uint8_t)((glob ? 1 : 0) | (len > 8 ? 2 : 0));
         for (int64_t k = 8; k < len; ++k) {
             ocol[optr[i] + k - 8] = (uint16_t)code(e0 + k);
             if (oval) oval[optr[i] + k - 8] = lv[e0 + k];
@@ -200,13 +203,14 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
         GS_HIP(hipMemcpyAsync(dch, hch, sizeof(int64_t) * 4 * kRegMaxChunks, hipMemcpyHostToDevice, s));
     }
     auto *ell = (uint4 *)c->buf("er_reg_ell").ensure(sizeof(uint4) * n);
+    auto *rflag = (uint8_t *)c->buf("er_reg_rflag").ensure((size_t)n + 64);
     double *ellv = ufast ? nullptr : (double *)c->buf("er_reg_ellv").ensure(sizeof(double) * 8 * n);
     auto *ocol = (uint16_t *)c->buf("er_reg_ocol").ensure(sizeof(uint16_t) * (nov + 1));
     double *oval = ufast ? nullptr : (double *)c->buf("er_reg_oval").ensure(sizeof(double) * (nov + 1));
     if (fresh) {
         k_ell8_fill<<<grid_for(n, 256, 8192), 256, 0, s>>>(0, (int32_t)n, T, dch, pad, G, NT == 256 ? 2 : 1,
                                                           ufast ? (int32_t)zs + 2 : -1, lp, li, lv, optr,
-                                                          ell, ellv, ocol, oval);
+                                                          ell, ellv, ocol, oval, rflag);
         GS_HIP(hipGetLastError());
         c->reg_ell_key = key;
     }
@@ -292,6 +296,8 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     A.rlen = rlen;
     A.ocol = ocol;
     A.oval = oval;
+    A.diag = diag;  // L_reg's diagonal (k_l_unit), read by the whole-column unit form
+    A.rflag = rflag;
 
     A.zslot = (int32_t)pad;
     A.maxiter = maxiter;
@@ -369,7 +375,7 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
         const int32_t zsh = hpt[h * kRegPartTab + 4 * kRegMaxChunks + 1];
         k_ell8_fill<<<grid_for(r1 - r0, 256, 8192), 256, 0, s>>>(
             r0, r1, pc0[h + 1] - pc0[h], dtab + h * 4 * kRegMaxChunks, (uint32_t)zsh, Gs, 1,
-            ufast ? zsh + 2 : -1, lp, li, lv, optr, ells, ellvs, ocols, ovals);
+            ufast ? zsh + 2 : -1, lp, li, lv, optr, ells, ellvs, ocols, ovals, nullptr);
         GS_HIP(hipGetLastError());
     }
     c->reg_split_key = skey;

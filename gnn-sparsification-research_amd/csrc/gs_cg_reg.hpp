@@ -48,6 +48,10 @@ static constexpr int kPre = GS_KPRE;
 #define GS_KPRE_P GS_KPRE
 #endif
 static constexpr int kPreP = GS_KPRE_P;
+// -DGS_CG_V2=0: the round-3 slot code of the whole-column unit form (A/B builds)
+#ifndef GS_CG_V2
+#define GS_CG_V2 1
+#endif
 // the one-wave form (k_cg_regres, hand-pipelined gathers) keeps its own, validated
 // distance: at 1 slot its results were wrong (tests m5-narrow, round 3)
 static constexpr int kPreN = 4;
@@ -83,6 +87,9 @@ struct RegArgs {
     int32_t *abortf;      // set when a hand-off poll gave up
     int32_t spinmax;      // wait budget of one hand-off poll, in ticks of the 100 MHz
                           // constant clock (wall_clock64); 0: give up at once
+    const double *diag;   // [n] L_reg's diagonal (unit form of the whole-column launch)
+    const uint8_t *rflag; // [n] bit 0: a p code of the row's ELL-8 entries is global (0x8000 |
+                          // row), bit 1: the row has more than 8 entries (k_ell8_fill)
     const int32_t *gate;  // optional: solve the columns only if *gate != 0 (the whole-column
                           // re-solve of a split tail whose hand-offs gave up; read once at
                           // launch, wave-uniform), else every column as usual

@@ -60,6 +60,13 @@ __device__ __forceinline__ double wide_readlane(double v, int ln) {
 template <int G, int R, bool UNIT, bool QR, bool SPLIT = false>
 __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     constexpr int CW = 64 / G;  // chains per wave
+    // V2 (whole columns, unit weights): each slot's "any p code global" and "any row
+    // longer than 8" tests are bits of two wave-uniform masks built once per launch (one
+    // scalar bit test per slot instead of a vector OR / compare / ballot), and the
+    // diagonal entry is loaded from L_reg's diagonal (one 8-B load instead of the entry
+    // count's load, convert and add) -- the same bits as the count-derived value, which
+    // is checked equal at setup for the unit form
+    constexpr bool V2 = GS_CG_V2 && UNIT && !SPLIT;
     extern __shared__ double lds[];
     const int part = SPLIT ? (int)(blockIdx.x % (unsigned)A.P) : 0;
     const int group = SPLIT ? (int)(blockIdx.x / (unsigned)A.P) : (int)blockIdx.x;
@@ -111,7 +118,11 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     // invariant, the compiler hoists all R of them out of the iteration loop and
     // keeps them live (hundreds of SGPRs/VGPRs, spilled to scratch).
     int ulds = 0;  // set below
-    auto launder = [&]() { asm volatile("" : "+v"(base), "+v"(uc), "+s"(ulds)); };
+    uint64_t gmask = 0, lmask = 0;  // V2 slot masks, set below
+    auto launder = [&]() {
+        asm volatile("" : "+v"(base), "+v"(uc), "+s"(ulds));
+        if constexpr (V2) asm volatile("" : "+s"(gmask), "+s"(lmask));
+    };
     const int ca_t = s_ch[t], keep_t = s_ch[2 * kRegMaxChunks + t], lbase_t = s_ch[3 * kRegMaxChunks + t];
     // slots u < ulds hold LDS-resident rows in every lane of the wave (a slot's rows are
     // 32 G consecutive rows of one chunk per lane group and the prefixes are whole
@@ -153,6 +164,9 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         __builtin_amdgcn_make_buffer_rsrc((void *)A.ell, 0, (int)(A.n * 16), 0x00020000);
     const __amdgpu_buffer_rsrc_t lrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)A.rlen, 0, (int)(A.n * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t drs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(V2 ? A.diag : nullptr), 0, (int)(V2 ? A.n * 8 : 0),
+                                          0x00020000);
     if (tid == 0) spl[zslot] = 0.0;
 
     // p of a row lives at its code: an LDS slot (< 0x8000) or 0x8000 | row (global);
@@ -194,7 +208,24 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     auto len_row = [&](int u) -> int {
         return (int)__builtin_amdgcn_raw_buffer_load_b16(lrs, base * 2, 64 * G * u, 0);
     };
+    auto diag_row = [&](int u) -> double {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(drs, base * 8, 256 * G * u, 0));
+    };
     auto rowof = [&](int u) { return base + 32 * G * u; };
+    // V2: bit u of gmask / lmask = some lane of this wave has a global p code / a row
+    // longer than 8 entries in slot u (rows of invalid slots contribute nothing)
+    // (laundered with the slot geometry: hoisted, their R bit tests would stay live as
+    // 2 R booleans across the iteration loop)
+    if constexpr (V2) {
+        // one slot at a time (once per launch): the loads of all slots in flight would keep
+        // 2 R ballots live at once
+        for (int u = 0; u < R; ++u) {
+            asm volatile("" : "+s"(gmask), "+s"(lmask));
+            const int f = u < uc ? (int)A.rflag[base + 32 * G * u] : 0;
+            if (__builtin_amdgcn_ballot_w64((f & 1) != 0)) gmask |= 1ull << u;
+            if (__builtin_amdgcn_ballot_w64((f & 2) != 0)) lmask |= 1ull << u;
+        }
+    }
 
     // q_i = (L_reg p)_i, SciPy csr_matvec: fold from 0.0 in ascending column, products
     // rounded; pown receives p_i.  Entries are p codes.  Unit form: off-diagonal
@@ -263,6 +294,46 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         return acc;
     };
 
+    // V2 slot u (u >= 0): dg = L_reg_ii loaded, the global fix-up and the long-row tail
+    // under the slot's mask bits; the arithmetic is spmv()'s, operation for operation
+    auto spmv2 = [&](int row, const uint4 e, double dg, double &pown, int u) -> double {
+        const bool fast = u < ulds;  // wave-uniform
+        const int self = fast ? 0 : code_of(row);
+        const uint32_t w4[4] = {e.x, e.y, e.z, e.w};
+        uint32_t ad[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ad[k] = (k & 1) ? wide_code_addr<1>(w4[k >> 1]) : wide_code_addr<0>(w4[k >> 1]);
+        pown = fast ? lds_at(lds0() + 256u * G * u) : ldc(self);
+        const double td = dg * pown;
+        spl[dslot] = -td;
+        double pv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) pv[k] = lds_at(ad[k]);
+        uint64_t gm = gmask;  // tested here, not hoisted (see launder)
+        asm volatile("" : "+s"(gm));
+        if ((gm >> u) & 1) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const bool gk = ad[k] >= 0x8000u * 8;
+                const double vg = __builtin_bit_cast(
+                    double, __builtin_amdgcn_raw_buffer_load_b64(prs, gk ? (int)(ad[k] & 0x3fff8u) + poff : kOob, 0, kAux));
+                pv[k] = gk ? vg : pv[k];
+            }
+            vm_drain();
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = acc - pv[k];
+        uint64_t lm = lmask;
+        asm volatile("" : "+s"(lm));
+        if ((lm >> u) & 1) {  // rows longer than 8 entries: ocol
+            const int64_t o0 = A.optr[row], o1 = A.optr[row + 1];
+            for (int64_t q = o0; q < o1; ++q) acc = acc - ldc((int)A.ocol[q]);
+            vm_drain();
+        }
+        return acc;
+    };
+
     // lanes 0..31 receive v of lanes 32..63 (v_permlane32_swap)
     auto upper_half = [](double v) -> double {
         const uint64_t b = (uint64_t)__double_as_longlong(v);
@@ -275,7 +346,25 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         double as[G], bs[G];
         as[0] = av;  // the folding lane's own row (g = 0)
         bs[0] = bv;
-        if (G == 2) {  // partner = lane + 32: one permlane swap per dword, no LDS
+        if (G == 2 && V2) {
+            // one swap per dword of (v, v): the returned vdst keeps the own value in lanes
+            // 0..31, the returned src holds lanes 32..63's there -- v is dead afterwards, so
+            // one copy per dword instead of two
+            auto sw = [](double v, double &own, double &part) {
+                const uint64_t b = (uint64_t)__double_as_longlong(v);
+                const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false);
+                const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+                own = __longlong_as_double((long long)(((uint64_t)hi[0] << 32) | lo[0]));
+                part = __longlong_as_double((long long)(((uint64_t)hi[1] << 32) | lo[1]));
+            };
+            sw(av, as[0], as[G - 1]);
+            if (same) {
+                bs[0] = as[0];
+                bs[G - 1] = as[G - 1];
+            } else {
+                sw(bv, bs[0], bs[G - 1]);
+            }
+        } else if (G == 2) {  // partner = lane + 32: one permlane swap per dword, no LDS
             as[G - 1] = upper_half(av);
             bs[G - 1] = same ? as[G - 1] : upper_half(bv);  // same: bv is av
         } else {
@@ -558,21 +647,26 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             {
                 launder();
                 double acc = 0.0;
-                uint4 eb[R];  // ELL rows and lengths, kPre slots ahead
+                uint4 eb[R];  // ELL rows and lengths (V2: diagonals), kPre slots ahead
                 int lb[R];
+                double db[R];
 #pragma unroll
                 for (int u = 0; u < kPre && u < R; ++u) {
                     eb[u] = ell_row(u);
-                    lb[u] = len_row(u);
+                    if constexpr (V2) db[u] = diag_row(u);
+                    else lb[u] = len_row(u);
                 }
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
                     if (u + kPre < R) {
                         eb[u + kPre] = ell_row(u + kPre);
-                        lb[u + kPre] = len_row(u + kPre);
+                        if constexpr (V2) db[u + kPre] = diag_row(u + kPre);
+                        else lb[u + kPre] = len_row(u + kPre);
                     }
                     double pv = 0.0, qv = 0.0;
-                    if (valid(u)) qv = spmv(rowof(u), eb[u], lb[u], pv, u);
+                    if constexpr (V2) {
+                        if (valid(u)) qv = spmv2(rowof(u), eb[u], db[u], pv, u);
+                    } else if (valid(u)) qv = spmv(rowof(u), eb[u], lb[u], pv, u);
                     if constexpr (QR) qr[u] = qv;
                     chain_step(acc, pv, qv, u);
                     __builtin_amdgcn_sched_barrier(0);
@@ -625,20 +719,25 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                 double acc = 0.0;
                 uint4 eb[R];
                 int lb[R];
+                double db[R];
 #pragma unroll
                 for (int u = 0; u < kPre && u < R; ++u) {
                     eb[u] = ell_row(u);
-                    lb[u] = len_row(u);
+                    if constexpr (V2) db[u] = diag_row(u);
+                    else lb[u] = len_row(u);
                 }
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
                     if (u + kPre < R) {
                         eb[u + kPre] = ell_row(u + kPre);
-                        lb[u + kPre] = len_row(u + kPre);
+                        if constexpr (V2) db[u + kPre] = diag_row(u + kPre);
+                        else lb[u + kPre] = len_row(u + kPre);
                     }
                     if (valid(u)) {
                         double pu;
-                        const double t2 = alpha * spmv(rowof(u), eb[u], lb[u], pu, u);
+                        const double q = V2 ? spmv2(rowof(u), eb[u], db[u], pu, u)
+                                            : spmv(rowof(u), eb[u], lb[u], pu, u);
+                        const double t2 = alpha * q;
                         r[u] = r[u] - t2;
                     }
                     chain_step(acc, r[u], r[u], u, true);

@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -156,6 +157,13 @@ struct gs_ctx {
     std::vector<gs::ProfPending> pending;
     gs::Graph g;
     gs::ErState er;
+    // symmetric Jaccard: the plan of the last call (graph epoch, part rows) kept with
+    // its task lists, so a repeated call plans nothing and does not wait for the host
+    std::vector<int64_t> jac_plan_key;
+    unsigned long long jac_plan_tot[8] = {};
+    std::vector<std::array<int64_t, 4>> jac_plan_bm;  // bitmap batches: g0, g1, task range
+    int64_t jac_bytes_epoch = -1;
+    double jac_bytes_sum = 0.0;
     std::vector<uint64_t> zig_key;  // (PCG64 state, stream length, block) of a parsed stream
     int64_t zig_draws = 0;          // draws known to cover it
     gs::DevBuf scratch[6];

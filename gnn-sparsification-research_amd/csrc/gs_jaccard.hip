@@ -604,14 +604,30 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts,
     JacSink sk{out, rev, counts, cc, cc ? c->buf("jac_opre").as<int64_t>() : nullptr, obase};
     double algo = 0.0;
     if (c->profiling) {
-        auto *acc = (unsigned long long *)c->buf("jac_bytes").ensure(8);
-        GS_HIP(hipMemsetAsync(acc, 0, 8, st));
-        k_jac_bytes<<<grid_for(n, 256, 4096), 256, 0, st>>>(ip, n, acc);
-        unsigned long long s = 0;
-        GS_HIP(hipMemcpyAsync(&s, acc, 8, hipMemcpyDeviceToHost, st));
-        GS_HIP(hipStreamSynchronize(st));
-        algo = (8.0 * (double)s + 12.0 * (double)nnz) * (nnz ? (double)(e1 - e0) / (double)nnz : 0.0);
+        if (c->jac_bytes_epoch != g.epoch) {  // sum of degrees^2, once per graph
+            auto *acc = (unsigned long long *)c->buf("jac_bytes").ensure(8);
+            GS_HIP(hipMemsetAsync(acc, 0, 8, st));
+            k_jac_bytes<<<grid_for(n, 256, 4096), 256, 0, st>>>(ip, n, acc);
+            unsigned long long s = 0;
+            GS_HIP(hipMemcpyAsync(&s, acc, 8, hipMemcpyDeviceToHost, st));
+            GS_HIP(hipStreamSynchronize(st));
+            c->jac_bytes_sum = (double)s;
+            c->jac_bytes_epoch = g.epoch;
+        }
+        algo = (8.0 * c->jac_bytes_sum + 12.0 * (double)nnz) * (nnz ? (double)(e1 - e0) / (double)nnz : 0.0);
     }
+    // the hash classes run concurrently on side streams (a class of big LDS tables
+    // fills one or two workgroups per CU; the others use the rest): each gets its own
+    // task lists; the bitmap class stays on the context stream
+    bool conc = true;
+    if (const char *e = getenv("GSPARSE_JAC_CONCURRENT")) conc = atoi(e) != 0;
+    // The plan (row classes, per-class task lists, bitmap batches) is a function of the
+    // graph and the part's rows only: a repeated call on the same rows launches the class
+    // kernels from the kept task lists -- no planning kernels, no host round trip.  (With
+    // the classes sharing one task-list buffer, GSPARSE_JAC_CONCURRENT=0, every call plans.)
+    const std::vector<int64_t> pkey = {g.epoch, r0, r1, n, nnz};
+    const bool cached = conc && c->jac_plan_key == pkey;
+    if (!cached) c->jac_plan_key.clear();
     hipEvent_t t0 = prof_begin(c);
     auto *cls = (int8_t *)c->buf("jac_cls").ensure(n);
     auto *ntask = (int32_t *)c->buf("jac_ntask").ensure(sizeof(int32_t) * n);
@@ -621,23 +637,23 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts,
     auto *goff = (int64_t *)c->buf("jac_goff").ensure(sizeof(int64_t) * (n + 1));
     constexpr int kTot = kJacClasses + 1;
     auto *dtot = (unsigned long long *)c->buf("jac_tot").ensure(8 * kTot);
-    GS_HIP(hipMemsetAsync(dtot, 0, 8 * kTot, st));
     const int64_t nr = r1 - r0;  // this part's rows: planned, task lists emitted
-    if (nr) k_jac_plan<<<grid_for(nr, 4, 4096), 256, 0, st>>>(ip, ix, r0, r1, cls, ntask, dtot);
+    if (!cached) {
+        GS_HIP(hipMemsetAsync(dtot, 0, 8 * kTot, st));
+        if (nr) k_jac_plan<<<grid_for(nr, 4, 4096), 256, 0, st>>>(ip, ix, r0, r1, cls, ntask, dtot);
+    }
     if (e1 > e0)
         k_jac_light<<<grid_for(e1 - e0, 256, 65536), 256, 0, st>>>(ip, ix, g.rows.as<int32_t>(), e0,
                                                                    e1, sk);
     GS_HIP(hipGetLastError());
-    unsigned long long htot[kTot];
-    GS_HIP(hipMemcpyAsync(htot, dtot, sizeof(htot), hipMemcpyDeviceToHost, st));
-    GS_HIP(hipStreamSynchronize(st));  // the only sync unless bitmap rows exist
+    unsigned long long *htot = c->jac_plan_tot;
+    if (!cached) {
+        GS_HIP(hipMemcpyAsync(htot, dtot, 8 * kTot, hipMemcpyDeviceToHost, st));
+        GS_HIP(hipStreamSynchronize(st));  // the only sync unless bitmap rows exist
+        c->jac_plan_bm.clear();
+    }
     int64_t tmax = 1;
     for (int k = 0; k < kJacClasses; ++k) tmax = (int64_t)htot[k] > tmax ? (int64_t)htot[k] : tmax;
-    // the hash classes run concurrently on side streams (a class of big LDS tables
-    // fills one or two workgroups per CU; the others use the rest): each gets its own
-    // task lists; the bitmap class stays on the context stream
-    bool conc = true;
-    if (const char *e = getenv("GSPARSE_JAC_CONCURRENT")) conc = atoi(e) != 0;
     if (conc) {
         for (auto &a : c->aux)
             if (!a) GS_HIP(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
@@ -656,18 +672,20 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts,
         const bool giant = k == kJacBitmap;
         const int64_t ntot = (int64_t)htot[k], ngiant = giant ? (int64_t)htot[kJacClasses] : 0;
         if (!ntot) continue;
-        GS_HIP(hipMemsetAsync(cnt + nr, 0, sizeof(int64_t), st));
-        GS_HIP(hipMemsetAsync(gfl + nr, 0, sizeof(int64_t), st));
-        k_jac_mask<<<grid_for(nr, 256, 16384), 256, 0, st>>>(cls, ntask, r0, r1, k, cnt,
-                                                             giant ? gfl : nullptr);
-        exclusive_scan_i64(c, cnt, off, nr + 1);
-        if (giant) exclusive_scan_i64(c, gfl, goff, nr + 1);
         int32_t *tslot = giant ? (int32_t *)c->buf("jac_tslot").ensure(sizeof(int32_t) * ntot)
                                : nullptr;
         int32_t *grow = giant ? (int32_t *)c->buf("jac_grow").ensure(sizeof(int32_t) * ngiant)
                               : nullptr;
-        k_jac_emit<<<grid_for(nr, 256, 16384), 256, 0, st>>>(cls, ntask, off, giant ? goff : nullptr,
-                                                             r0, r1, k, trow, ti, tslot, grow);
+        if (!cached) {
+            GS_HIP(hipMemsetAsync(cnt + nr, 0, sizeof(int64_t), st));
+            GS_HIP(hipMemsetAsync(gfl + nr, 0, sizeof(int64_t), st));
+            k_jac_mask<<<grid_for(nr, 256, 16384), 256, 0, st>>>(cls, ntask, r0, r1, k, cnt,
+                                                                 giant ? gfl : nullptr);
+            exclusive_scan_i64(c, cnt, off, nr + 1);
+            if (giant) exclusive_scan_i64(c, gfl, goff, nr + 1);
+            k_jac_emit<<<grid_for(nr, 256, 16384), 256, 0, st>>>(cls, ntask, off, giant ? goff : nullptr,
+                                                                 r0, r1, k, trow, ti, tslot, grow);
+        }
         GS_HIP(hipGetLastError());
         GS_CHECK(ntot <= INT32_MAX, GS_EUNSUPPORTED, "too many Jaccard tasks (%lld)", (long long)ntot);
         // every emitted task is this part's (only its rows were planned)
@@ -691,26 +709,34 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts,
         } else if (k == 3) {
             k_jac_hash<32768><<<nb, 1024, 0, hs>>>(ip, ix, ntask, trow, ti, tlo, sk);
         } else {
-            // bitmaps in batches of rows (<= 1 GiB of bits at a time)
+            // bitmaps in batches of rows (<= 1 GiB of bits at a time); the batches' task
+            // ranges are part of the kept plan
             const int64_t words = (n + 31) / 32;
             int64_t per = ((int64_t)1 << 30) / (4 * words);
             if (per < 1) per = 1;
-            std::vector<int32_t> hrow(ngiant);
-            GS_HIP(hipMemcpyAsync(hrow.data(), grow, sizeof(int32_t) * ngiant,
-                                  hipMemcpyDeviceToHost, st));
-            GS_HIP(hipStreamSynchronize(st));
-            for (int64_t g0 = 0; g0 < ngiant; g0 += per) {
-                const int64_t g1 = g0 + per < ngiant ? g0 + per : ngiant;
-                // task range of rows hrow[g0 .. g1): tasks are in row order
-                int64_t tb[2];
-                GS_HIP(hipMemcpyAsync(&tb[0], off + (hrow[g0] - r0), 8, hipMemcpyDeviceToHost, st));
-                if (g1 < ngiant)
-                    GS_HIP(hipMemcpyAsync(&tb[1], off + (hrow[g1] - r0), 8, hipMemcpyDeviceToHost, st));
+            if (!cached) {
+                std::vector<int32_t> hrow(ngiant);
+                GS_HIP(hipMemcpyAsync(hrow.data(), grow, sizeof(int32_t) * ngiant,
+                                      hipMemcpyDeviceToHost, st));
                 GS_HIP(hipStreamSynchronize(st));
-                if (g1 >= ngiant) tb[1] = ntot;
-                // this part's tasks only
-                if (tb[0] < tlo) tb[0] = tlo;
-                if (tb[1] > thi) tb[1] = thi;
+                for (int64_t g0 = 0; g0 < ngiant; g0 += per) {
+                    const int64_t g1 = g0 + per < ngiant ? g0 + per : ngiant;
+                    // task range of rows hrow[g0 .. g1): tasks are in row order
+                    int64_t tb[2];
+                    GS_HIP(hipMemcpyAsync(&tb[0], off + (hrow[g0] - r0), 8, hipMemcpyDeviceToHost, st));
+                    if (g1 < ngiant)
+                        GS_HIP(hipMemcpyAsync(&tb[1], off + (hrow[g1] - r0), 8, hipMemcpyDeviceToHost, st));
+                    GS_HIP(hipStreamSynchronize(st));
+                    if (g1 >= ngiant) tb[1] = ntot;
+                    // this part's tasks only
+                    if (tb[0] < tlo) tb[0] = tlo;
+                    if (tb[1] > thi) tb[1] = thi;
+                    c->jac_plan_bm.push_back({g0, g1, tb[0], tb[1]});
+                }
+            }
+            for (const auto &bb : c->jac_plan_bm) {
+                const int64_t g0 = bb[0], g1 = bb[1];
+                const int64_t tb[2] = {bb[2], bb[3]};
                 if (tb[1] <= tb[0]) continue;
                 auto *bm = (uint32_t *)c->buf("jac_bitmap").ensure(sizeof(uint32_t) * words * (g1 - g0));
                 GS_HIP(hipMemsetAsync(bm, 0, sizeof(uint32_t) * words * (g1 - g0), st));
@@ -730,6 +756,7 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts,
             GS_HIP(hipEventRecord(c->aux_ev[k], c->aux[k]));
             GS_HIP(hipStreamWaitEvent(st, c->aux_ev[k], 0));
         }
+    if (!cached && conc) c->jac_plan_key = pkey;
     prof_end(c, t0, counts ? "common_neighbors" : "jaccard", algo);
 }
 

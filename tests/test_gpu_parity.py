@@ -610,6 +610,48 @@ def test_exact_er_through_sparsifier(gs):
     assert m.dtype == torch.bool and int(m.sum()) > 0
 
 
+@pytest.mark.parametrize("name", exact_er_names())
+def test_exact_er_kept_sets_vs_reference(gs, name):
+    """sparsify("effective_resistance", r) kept sets (core.py:229-240) vs the
+    reference's own mask of its golden scores: identical for every column whose
+    reference score lies outside the reference's pinv noise band (2 x
+    EXACT_ER_ATOL) around the cut, and the same kept count; against the lifted
+    oracle's scores (the same inverse up to ~cond * eps) the band is 1e-7 relative."""
+    import scipy.sparse as sp
+
+    g = load_golden(name)
+    n = int(g["num_nodes"])
+    ref = exact_er_golden(name)
+    E = g["edge_index"].shape[1] if "edge_index" in g else len(ref)
+    if "edge_index" in g:
+        sp_, _ = make(gs, g, with_x=False)
+        got_scores = sp_.compute_scores("effective_resistance")
+    else:
+        adj = sp.csr_matrix((g["data"], g["indices"], g["indptr"]), shape=(n, n))
+        got_scores = gs.calculate_effective_resistance_scores(adj)
+        sp_ = None
+    lifted = O.exact_er(g["indptr"], g["indices"], g["data"], n, lifted=True)
+    for r in (0.9, 0.6, 0.5, 0.2):
+        for low in (False, True):
+            k = int(E * r)
+            if sp_ is not None:
+                _, m = sp_.sparsify("effective_resistance", r, return_mask=True, keep_lowest=low)
+                m = m.numpy()
+            else:
+                m = O.topk_mask(got_scores, E, r, low)
+            assert int(m.sum()) == k
+            for scores, band in ((ref, 2 * EXACT_ER_ATOL), (lifted, 1e-7 * float(np.max(lifted)))):
+                rm = O.topk_mask(scores, E, r, low)
+                if k == 0:  # the idx[-0:] quirk: every scored column (top) or none (lowest)
+                    assert np.array_equal(m, rm)
+                    continue
+                srt = np.sort(scores)
+                cut = srt[k - 1] if low else srt[len(srt) - k]
+                clear = np.abs(scores - cut) > band
+                clear = np.concatenate([clear, np.zeros(E - len(scores), dtype=bool)])
+                assert np.array_equal(m[clear], rm[clear]), (name, r, low, int((m != rm)[clear].sum()))
+
+
 @pytest.mark.parametrize("n,blocks", [(3000, 5), (4100, 1), (70, 3)])
 def test_exact_er_components_and_padding(gs, n, blocks):
     """Several components (plus isolated nodes), weights, n not a multiple of 64."""
