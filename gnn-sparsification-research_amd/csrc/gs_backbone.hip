@@ -113,14 +113,20 @@ __global__ void k_bb_srckeys(const int64_t *__restrict__ src, int64_t E, uint64_
 }
 
 // 2-hop witness. state: 0 = unresolved, 1 = keep, 2 = prune.
+// Only the columns of this part (source row u % nparts == part) are decided here:
+// the other parts' columns are never read by this part (k_bb_need, k_bb_keep).
 __global__ void k_bb_witness(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
                              const double *__restrict__ w, int64_t E,
                              const int64_t *__restrict__ gp, const int32_t *__restrict__ gi,
-                             const double *__restrict__ gw, double eps,
+                             const double *__restrict__ gw, double eps, int part, int nparts,
                              uint8_t *__restrict__ state) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
          i += (int64_t)gridDim.x * blockDim.x) {
         int64_t u = src[i], v = dst[i];
+        if (nparts > 1 && u % nparts != part) {
+            state[i] = 3;  // another part's column: not decided here
+            continue;
+        }
         double wi = w[i];
         if (u == v) {  // d(u,u) = 0
             state[i] = (wi <= 0.0 + eps) ? 1 : 2;
@@ -787,7 +793,7 @@ __global__ void k_bb_certify(const int64_t *__restrict__ src, const int64_t *__r
                              uint8_t *__restrict__ state) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
          i += (int64_t)gridDim.x * blockDim.x) {
-        if (state[i] != 0) continue;
+        if (state[i] != 0) continue;  // decided, or another part's column (3)
         const int64_t u = src[i], v = dst[i];
         const double wi = w[i];
         const int64_t du = gp[u + 1] - gp[u], dv = gp[v + 1] - gp[v];
@@ -1043,7 +1049,7 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
         unsigned long long *misc = (unsigned long long *)b_misc.ensure(64);
         GS_HIP(hipMemsetAsync(misc, 0, 64, s));
         int64_t relax = 0;
-        hipEvent_t t0 = prof_begin(c);
+        hipEvent_t t0 = prof_begin(c), tall = prof_begin(c);
         if (E > 0) {
             int64_t *gp;
             int32_t *gi;
@@ -1060,8 +1066,12 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
             exclusive_scan_i64(c, (const int64_t *)deg, optr, n + 1);
             // 2-hop witness
             uint8_t *state = (uint8_t *)b_state.ensure(E);
+            prof_end(c, t0, "bb_build", 0.0);
+            hipEvent_t tp = prof_begin(c);
             k_bb_witness<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, dw, E, gp, gi, gw, eps,
-                                                               state);
+                                                               part, nparts, state);
+            prof_end(c, tp, "bb_witness", 0.0);
+            tp = prof_begin(c);
             // landmark / degree-1 certificates (GSPARSE_BB_LANDMARKS = K, 0 = off)
             int K = 16;
             if (const char *e = getenv("GSPARSE_BB_LANDMARKS")) K = atoi(e) < 0 ? 0 : atoi(e);
@@ -1102,6 +1112,8 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                                                                    lcomp, K, eps, mrg, state);
                 GS_HIP(hipGetLastError());
             }
+            prof_end(c, tp, "bb_certify", 0.0);
+            tp = prof_begin(c);
             // sources needing a search
             int64_t *flag = (int64_t *)b_flag.ensure(8 * (n + 1));
             int64_t *pos = (int64_t *)b_pos.ensure(8 * (n + 1));
@@ -1180,13 +1192,14 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                 }
                 GS_HIP(hipGetLastError());
             }
+            prof_end(c, tp, "bb_search", 0.0);
             k_bb_keep<<<grid_for(E, 256, 8192), 256, 0, s>>>(state, dsrc, E, part, nparts, dkeep);
             unsigned long long hr = 0;
             GS_HIP(hipMemcpyAsync(&hr, misc + 1, 8, hipMemcpyDeviceToHost, s));
             GS_HIP(hipStreamSynchronize(s));
             relax = (int64_t)hr;
         }
-        prof_end(c, t0, "metric_backbone", 12.0 * (double)relax + 9.0 * (double)E);
+        prof_end(c, tall, "metric_backbone", 12.0 * (double)relax + 9.0 * (double)E);
         finish_out(c, keep, dkeep, E, keep_loc);
         if (n_relax) *n_relax = relax;
     });

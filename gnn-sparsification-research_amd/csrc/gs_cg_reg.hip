@@ -219,8 +219,10 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     // (GSPARSE_REG_QR=1: q kept in registers from the SpMV pass, x read-modify-written
     // in Xc every iteration -- ~6x the fabric traffic for a wash in time).
     // The split form always keeps q in registers (its x lives in Xc).
+    // (round 3 measured the whole-column q-in-registers form -- x read-modify-written in
+    // Xc every iteration -- at parity with x in registers and 6x the fabric traffic; it
+    // is no longer built, GSPARSE_REG_QR is ignored)
     A.qreg = 0;
-    if (const char *e = getenv("GSPARSE_REG_QR")) A.qreg = atoi(e) != 0;
     // Split plan: the last round of columns, when it leaves at least half the CUs idle,
     // runs as groups of P workgroups per column (k_cg_regwide<..., SPLIT>), each part a
     // contiguous range of the BLAS chunks with all its rows' p in LDS.

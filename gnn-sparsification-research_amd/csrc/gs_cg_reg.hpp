@@ -52,6 +52,10 @@ static constexpr int kPreP = GS_KPRE_P;
 #ifndef GS_CG_V2
 #define GS_CG_V2 1
 #endif
+// V2 p update: slots past the LDS prefix handled in groups of this many (one wait each)
+#ifndef GS_PGRP
+#define GS_PGRP 4
+#endif
 // the one-wave form (k_cg_regres, hand-pipelined gathers) keeps its own, validated
 // distance: at 1 slot its results were wrong (tests m5-narrow, round 3)
 static constexpr int kPreN = 4;

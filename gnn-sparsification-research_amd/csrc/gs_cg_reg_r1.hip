@@ -1,0 +1,7 @@
+// gs_cg_reg_r1.hip -- instantiations of k_cg_regres (the 256-thread form) with 1 thread(s)
+// per chain (gs_cg_reg.hpp); a file of its own so it builds in parallel with gs_cg_reg_g1.hip.
+#include "gs_cg_reg.hpp"
+
+namespace gs {
+GS_REGRES_LAUNCH_DEF(1)
+}  // namespace gs

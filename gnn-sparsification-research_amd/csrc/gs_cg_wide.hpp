@@ -594,6 +594,44 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                         __builtin_amdgcn_sched_barrier(0);
                     }
                     launder();
+                    if constexpr (V2 && GS_PGRP > 0) {
+                        // the slots past the prefix in groups of GS_PGRP: all their p_old loads (LDS
+                        // or the global rows) issued, one wait, then the updates -- one memory
+                        // round trip per group instead of one per slot
+                        constexpr int kGrp = GS_PGRP;
+#pragma unroll
+                        for (int u0 = 0; u0 < R; u0 += kGrp) {
+                            if (u0 + kGrp <= ulds) continue;  // wave-uniform: the group is in the prefix
+                            double pog[kGrp > 0 ? kGrp : 1];
+#pragma unroll
+                            for (int k = 0; k < kGrp; ++k) {
+                                const int u = u0 + k;
+                                if (u >= R) break;
+                                const int cd = code_of(rowof(u));
+                                const bool gl = cd >= 0x8000 && u >= ulds && valid(u);
+                                const double lv = spl[cd < 0x8000 ? cd : zslot];
+                                const double gv = __builtin_bit_cast(
+                                    double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                prs, gl ? (cd & 0x7fff) * 8 + poff : kOob, 0, kAux));
+                                pog[k] = cd < 0x8000 ? lv : gv;
+                            }
+                            vm_drain();
+#pragma unroll
+                            for (int k = 0; k < kGrp; ++k) {
+                                const int u = u0 + k;
+                                if (u >= R) break;
+                                if (u >= ulds && valid(u)) {
+                                    const double po = pog[k];
+                                    if constexpr (!QR) {
+                                        const double t1 = alpha_prev * po;
+                                        x[u] = x[u] + t1;
+                                    }
+                                    const double pb = po * beta;
+                                    pstore(u, pb + r[u]);
+                                }
+                            }
+                        }
+                    } else {
 #pragma unroll
                     for (int u = 0; u < R; ++u) {
                         if (u >= ulds && valid(u)) {
@@ -605,6 +643,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                             const double pb = po * beta;
                             pstore(u, pb + r[u]);
                         }
+                    }
                     }
                 } else
 #pragma unroll
@@ -822,8 +861,8 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                 else go(k_cg_regwide<G_, 44, false, Q>);                                      \
             }                                                                                 \
         };                                                                                    \
-        if (A.qreg) pick(std::true_type{});                                                   \
-        else pick(std::false_type{});                                                         \
+        (void)A.qreg; /* whole columns keep x in registers (the q-in-registers form of */     \
+        pick(std::false_type{}); /* round 2 lives on only in the split tail) */               \
     }
 
 // one launch of the split form (q in registers), grid = groups x A.P workgroups

@@ -29,7 +29,11 @@ static constexpr int64_t kJacGiant = 16384;
 static constexpr int64_t kJacTaskMin = 65536;
 static constexpr int kJacClasses = 5;  // 4 LDS table sizes + bitmap
 static constexpr int kJacBitmap = 4;
-static constexpr int kJacUnroll = 4;   // list elements per lane in flight
+static constexpr int kJacUnrollDef = 4;  // list elements per lane in flight
+// the big-table classes run 1-2 workgroups per CU: more list loads in flight per lane
+#ifndef GS_JAC_UNROLL_BIG
+#define GS_JAC_UNROLL_BIG 8
+#endif
 static constexpr int kJacMaxEnt = 1024;  // entries per task (LDS staging)
 static constexpr int64_t kJacSmall = 16;  // d_v <= this: 16-lane groups
 
@@ -387,7 +391,7 @@ struct JacBitProbe {
 
 // Probe phase shared by the LDS-table and bitmap kernels (after jac_stage and
 // a barrier).  The d_u of the owner and each entry's d_v give the union.
-template <class Probe>
+template <class Probe, int kJacUnroll = kJacUnrollDef>
 __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix, int64_t du,
                                                  int64_t lo, const JacStage &st,
                                                  const JacSink &sk, const Probe &pr) {
@@ -476,7 +480,8 @@ __global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ i
         }
     }
     __syncthreads();
-    jac_probe_staged(ix, du, lo, st, sk, JacHashProbe{tab, shift, mask});
+    constexpr int U = C >= 16384 ? GS_JAC_UNROLL_BIG : kJacUnrollDef;
+    jac_probe_staged<JacHashProbe, U>(ix, du, lo, st, sk, JacHashProbe{tab, shift, mask});
 }
 
 __global__ void k_jac_bitmap_build(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,

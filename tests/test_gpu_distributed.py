@@ -169,6 +169,18 @@ def test_nccl_sharded_scorers_equal_single_gpu(gs, nccl_world1):
 
     keep = sharded_backbone(comm, ei, n, w)
     assert np.array_equal(keep, backbone_mask(ei, n, w, 1e-9))
+    # the global top-k on the device after the all-gather (sharded_sparsify)
+    from gsparse.distributed import sharded_sparsify
+
+    E = ei.shape[1]
+    jd = sharded_edge_scores(e, comm, "jaccard")
+    for r in (0.9, 0.5, 0.1):
+        m, info = sharded_sparsify(e, comm, jd, E, r, tie_break="stable")
+        assert m.is_cuda and m.dtype == torch.bool
+        ref = O.topk_mask(jd.cpu().numpy(), E, r, False, kind="stable")
+        assert np.array_equal(m.cpu().numpy(), ref), r
+        mn, _ = sharded_sparsify(e, comm, jd, E, r, tie_break="numpy")
+        assert np.array_equal(mn.cpu().numpy(), O.topk_mask(jd.cpu().numpy(), E, r, False)), r
 
 
 def _gloo_rank(rank, world, port, q):
@@ -185,14 +197,20 @@ def _gloo_rank(rank, world, port, q):
         data = gsparse.Data(edge_index=torch.from_numpy(ei), num_nodes=n)
         e = gsparse.GraphSparsifier(data, "cuda:0")._engine
         comm = Comm()
-        jac = sharded_edge_scores(e, comm, "jaccard").numpy()
+        jac_t = sharded_edge_scores(e, comm, "jaccard")
+        jac = jac_t.numpy()
+        from gsparse.distributed import sharded_sparsify
+
+        E = ei.shape[1]
+        masks = {r: sharded_sparsify(e, comm, jac_t, E, r, tie_break="stable")[0].numpy().copy()
+                 for r in (0.8, 0.5, 0.2)}
         n2 = 12000
         ei2 = graphs.roman_like(n2, 17500, seed=3)
         e2 = gsparse.GraphSparsifier(gsparse.Data(edge_index=torch.from_numpy(ei2), num_nodes=n2),
                                      "cuda:0")._engine
         er = sharded_approx_er(e2, comm, epsilon=0.9, max_cg_iters=60, blas_threads=8).numpy()
         if rank == 0:
-            q.put((jac, er))
+            q.put((jac, er, masks))
     finally:
         dist.destroy_process_group()
 
@@ -213,13 +231,22 @@ def test_ranks_sharing_the_gpu_over_gloo(gs, world, monkeypatch):
     procs = [ctx.Process(target=_gloo_rank, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    jac, er = q.get(timeout=300)
+    jac, er, masks = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     ei, n = _hub_graph()
     ip, ix, _ = O.canonical_csr(ei, n)
-    assert bits_equal(jac, O.jaccard(ip, ix))
+    ref = O.jaccard(ip, ix)
+    assert bits_equal(jac, ref)
+    # the global top-k after the exchange (core.py:229-240): N-rank kept set == one GPU
+    # == np.argsort(kind='stable') of the reference's scores
+    e1 = _engine(gs, ei, n)
+    for r, m in masks.items():
+        E = ei.shape[1]
+        single, *_ = e1.topk_mask(ref, E, int(E * r), False)
+        assert np.array_equal(m, single), r
+        assert np.array_equal(m, O.topk_mask(ref, E, r, False, kind="stable")), r
     n2 = 12000
     ei2 = graphs.roman_like(n2, 17500, seed=3)
     e2 = _engine(gs, ei2, n2)

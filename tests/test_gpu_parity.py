@@ -639,7 +639,7 @@ def test_exact_er_kept_sets_vs_reference(gs, name):
                 m = m.numpy()
             else:
                 m = O.topk_mask(got_scores, E, r, low)
-            assert int(m.sum()) == k
+            assert int(m.sum()) == (k if k else (0 if low else len(ref)))  # k == 0: idx[-0:]
             for scores, band in ((ref, 2 * EXACT_ER_ATOL), (lifted, 1e-7 * float(np.max(lifted)))):
                 rm = O.topk_mask(scores, E, r, low)
                 if k == 0:  # the idx[-0:] quirk: every scored column (top) or none (lowest)

@@ -51,6 +51,10 @@ def run(part, nparts, keep):
              GS_DEVICE, 1e-9, part, nparts, keep.data_ptr(), GS_DEVICE, ctypes.byref(relax))
 
 
+PHASES = ("bb_build", "bb_witness", "bb_certify", "bb_search")
+phase_ms = {}
+
+
 def timed(fn):
     ctx.profile(True)
     ctx.profile_reset()
@@ -59,6 +63,8 @@ def timed(fn):
     ctx.synchronize()
     p = ctx.profile_read()
     ctx.profile(False)
+    phase_ms.clear()
+    phase_ms.update({k: round(p[k]["ms"] / p[k]["launches"], 2) for k in PHASES if k in p})
     return p["metric_backbone"]["ms"] / p["metric_backbone"]["launches"]
 
 
@@ -66,20 +72,22 @@ whole = torch.empty(E, dtype=torch.uint8, device=dev)
 run(0, 1, whole)  # warm-up
 out = {"workload": f"RMAT-{scale} metric backbone, one rank's work per part", "E": E,
        "graph_gen_s": round(gen, 2), "whole_ms": round(timed(lambda: run(0, 1, whole)), 2),
-       "kept": int(whole.sum().item()), "per_n": {}}
+       "kept": int(whole.sum().item()), "whole_phases_ms": dict(phase_ms), "per_n": {}}
 print(json.dumps({"whole_ms": out["whole_ms"]}), flush=True)
 for N in (2, 4, 8):
-    parts, rel = [], []
+    parts, rel, phases = [], [], []
     tot = torch.zeros(E, dtype=torch.int32, device=dev)
     for r in range(N):
         k = torch.empty(E, dtype=torch.uint8, device=dev)
         parts.append(timed(lambda: run(r, N, k)))
         rel.append(relax.value)
+        phases.append(dict(phase_ms))
         tot += k.to(torch.int32)
     same = bool(torch.equal(tot.to(torch.uint8), whole)) and int(tot.max().item()) <= 1
     mean = sum(parts) / N
     out["per_n"][N] = {"part_ms": [round(x, 2) for x in parts], "max_part_ms": round(max(parts), 2),
                        "max_over_mean": round(max(parts) / mean, 4), "relaxations": rel,
+                       "phases_ms_part0": phases[0],
                        "sum_equals_whole": same}
     print(json.dumps({N: out["per_n"][N]}), flush=True)
 print(json.dumps(out), flush=True)
