@@ -30,8 +30,20 @@ static int bits_for_bb(uint64_t v) {
 
 static constexpr uint64_t kInfBits = 0x7ff0000000000000ull;
 static constexpr int kBbLandmarkRounds = 256;  // frontier rounds per landmark search
-static constexpr uint32_t kQMaskTouched = 0x80000000u;  // k_bb_sssp_multi: node in the reset list
-static constexpr uint32_t kQMaskSources = 0x7fffffffu;
+// k_bb_sssp_multi's per-node mask: bits 0-7 the sources queued in the next frontier,
+// 8-15 the sources for which the node waits in the far pile, 30 the node is in the
+// far list, 31 in the reset list
+static constexpr uint32_t kQMaskTouched = 0x80000000u;
+static constexpr uint32_t kQMaskFarListed = 0x40000000u;
+static constexpr uint32_t kQMaskSources = 0xffu;
+static constexpr int kQMaskFarShift = 8;
+// k_bb_sssp_multi: frontier nodes with more entries than this are expanded by the
+// whole workgroup (at most kBbHeavyMax of them per round; the rest as usual)
+#ifndef GS_BB_HEAVY
+#define GS_BB_HEAVY 1024
+#endif
+static constexpr int64_t kBbHeavy = GS_BB_HEAVY;
+static constexpr int kBbHeavyMax = 256;
 
 // osrc/odst: the caller's ids (which columns are s < d: metric_backbone.py:70-79
 // builds G from those); src/dst: the (possibly relabeled) ids G is built in
@@ -430,6 +442,14 @@ __device__ __forceinline__ void bb_block_max_s(unsigned long long (&m)[S], unsig
 // sources whose label of x improved in the round (x is queued once).  Each
 // source keeps its own bound s_wmax[s], lowered by its own targets exactly as
 // in k_bb_sssp, so every source reaches the same fixpoint as alone.
+// Near-far order (delta > 0): an improvement to a label >= the source's
+// threshold s_thr[s] waits in the far pile instead of the next frontier; when
+// a source has nothing near left its threshold moves to (least pending far
+// label) + delta and the far labels below it join the frontier.  Labels are
+// then mostly expanded once at their final value (a plain frontier search
+// re-expands ~1.9x as many on RMAT-18's Jaccard costs; near-far ~1.05x at
+// delta = median weight / 2, tools/bb_nearfar_sim.c) -- the fixpoint, and so
+// every distance and decision, is the same in any order.
 template <int NT, int S>
 __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     const int64_t *__restrict__ gp, const int32_t *__restrict__ gi, const double *__restrict__ gw,
@@ -438,12 +458,15 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     const double *__restrict__ w, double eps, uint8_t *__restrict__ state,
     unsigned long long *__restrict__ dist_all, uint32_t *__restrict__ qmask_all,
     int32_t *__restrict__ fr_all, uint32_t *__restrict__ fm_all, int32_t *__restrict__ touched_all,
-    unsigned long long *__restrict__ relax_total) {
+    int32_t *__restrict__ far_all, double delta, unsigned long long *__restrict__ relax_total) {
     static_assert(S >= 1 && S <= 8, "1..8 sources per workgroup");
     constexpr int NW = NT / 64;
-    __shared__ int s_fcount, s_ncount, s_tcount;
-    __shared__ double s_wmax[S];
-    __shared__ unsigned long long s_wkey[S];
+    __shared__ int s_fcount, s_ncount, s_tcount, s_nfar, s_nfar2, s_farleft, s_nheavy;
+    __shared__ int32_t s_heavy[kBbHeavyMax];
+    __shared__ uint32_t s_hmask[kBbHeavyMax];
+    __shared__ uint32_t s_nearany;
+    __shared__ double s_wmax[S], s_thr[S];
+    __shared__ unsigned long long s_wkey[S], s_farmin[S];
     __shared__ int64_t s_src[S];
     __shared__ unsigned long long s_relax;
     __shared__ int32_t w_pre[NW][65];
@@ -456,7 +479,9 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     int32_t *fb = fa + n;
     uint32_t *fm = fm_all + (int64_t)blockIdx.x * n;
     int32_t *touched = touched_all + (int64_t)blockIdx.x * n;
+    int32_t *farA = far_all + (int64_t)blockIdx.x * 2 * n, *farB = farA + n;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const double thr0 = delta > 0.0 ? delta : __longlong_as_double((long long)kInfBits);
     if (threadIdx.x == 0) s_relax = 0;
     unsigned long long relax = 0;
     const int64_t nbatch = (nsrc + S - 1) / S;
@@ -465,6 +490,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
             const int64_t si = bi * S + threadIdx.x;
             s_src[threadIdx.x] = si < nsrc ? sources[si] : -1;
             s_wkey[threadIdx.x] = 0ull;
+            s_thr[threadIdx.x] = thr0;
+            s_farmin[threadIdx.x] = kInfBits;
         }
         __syncthreads();
         // largest unresolved target weight of each source (none: nothing to decide)
@@ -503,17 +530,37 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
             s_fcount = f;
             s_ncount = 0;
             s_tcount = f;
+            s_nfar = 0;
+            s_farleft = 0;
+            s_nearany = 0;
         }
         __syncthreads();
         int32_t *cur = fa, *nxt = fb;
+        uint32_t nearacc = 0;  // sources this lane queued near in the round
         while (true) {
             const int fc = s_fcount;
-            if (fc == 0) break;
+            if (fc == 0 && !s_farleft) break;
             double wmax[S];
 #pragma unroll
             for (int k = 0; k < S; ++k) wmax[k] = s_wmax[k];
-            for (int f = threadIdx.x; f < fc; f += NT)
-                fm[f] = atomicAnd(&qmask[cur[f]], kQMaskTouched) & kQMaskSources;
+            if (threadIdx.x == 0) s_nheavy = 0;
+            __syncthreads();
+            // heavy frontier nodes (more than kBbHeavy entries: the R-MAT hubs) are taken
+            // out of the per-wave chunks and expanded by the whole workgroup below, so one
+            // wave does not walk a hub's list while the others wait at the barrier
+            for (int f = threadIdx.x; f < fc; f += NT) {
+                const int32_t x = cur[f];
+                uint32_t m = atomicAnd(&qmask[x], ~kQMaskSources) & kQMaskSources;
+                if (m && gp[x + 1] - gp[x] > kBbHeavy) {
+                    const int h = atomicAdd(&s_nheavy, 1);
+                    if (h < kBbHeavyMax) {
+                        s_heavy[h] = x;
+                        s_hmask[h] = m;
+                        m = 0;
+                    }
+                }
+                fm[f] = m;
+            }
             __syncthreads();
             for (int f0 = wv * 64; f0 < fc; f0 += NT) {
                 const int f = f0 + lane;
@@ -522,9 +569,9 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                 uint32_t m = 0;
                 if (f < fc) {
                     const int32_t x = cur[f];
-                    b = gp[x];
-                    deg = (int)(gp[x + 1] - b);
                     m = fm[f];
+                    b = gp[x];
+                    deg = m ? (int)(gp[x + 1] - b) : 0;
 #pragma unroll
                     for (int k = 0; k < S; ++k)
                         w_d[wv][lane][k] = __longlong_as_double((long long)__hip_atomic_load(
@@ -576,7 +623,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                                            : 0ull;
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
-                    uint32_t imp = 0;
+                    uint32_t imp = 0, fimp = 0;
 #pragma unroll
                     for (int k = 0; k < S; ++k) {
                         if (!((mm[u] >> k) & 1u)) continue;
@@ -586,20 +633,89 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                         const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
                         if (nb >= cd[u][k]) continue;
                         const unsigned long long old = atomicMin(&dist[(int64_t)y[u] * S + k], nb);
-                        if (nb < old) imp |= 1u << k;
+                        if (nb < old) {
+                            if (nd < s_thr[k]) {  // LDS: read on improvements only
+                                imp |= 1u << k;
+                            } else {
+                                fimp |= 1u << (kQMaskFarShift + k);
+                                atomicMin(&s_farmin[k], nb);
+                            }
+                        }
                     }
-                    if (imp) {  // queue y once per round (the top bit is the touched flag)
-                        const uint32_t om = atomicOr(&qmask[y[u]], imp);
-                        if ((om & kQMaskSources) == 0) {
+                    if (imp | fimp) {  // queue y once per round; far: list it once, reset list
+                        const uint32_t add = fimp ? (imp | fimp | kQMaskFarListed | kQMaskTouched) : imp;
+                        const uint32_t om = atomicOr(&qmask[y[u]], add);
+                        if (imp && (om & kQMaskSources) == 0) {
                             const int q = atomicAdd(&s_ncount, 1);
                             nxt[q] = y[u];
                         }
+                        if (fimp && !(om & kQMaskFarListed)) farA[atomicAdd(&s_nfar, 1)] = y[u];
+                        if (fimp && !(om & kQMaskTouched)) touched[atomicAdd(&s_tcount, 1)] = y[u];
+                        nearacc |= imp;
                     }
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            {
+                const int nh = s_nheavy < kBbHeavyMax ? s_nheavy : kBbHeavyMax;
+                for (int h = 0; h < nh; ++h) {
+                    const int32_t x = s_heavy[h];
+                    const uint32_t m = s_hmask[h];
+                    double dx[S];
+#pragma unroll
+                    for (int k = 0; k < S; ++k)
+                        dx[k] = ((m >> k) & 1u) ? __longlong_as_double((long long)__hip_atomic_load(
+                                                      &dist[(int64_t)x * S + k], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP))
+                                                : 0.0;
+                    const int64_t e1 = gp[x + 1];
+                    for (int64_t e = gp[x] + threadIdx.x; e < e1; e += NT) {
+                        const int32_t y = gi[e];
+                        const double we = gw[e];
+                        unsigned long long cd[S];
+#pragma unroll
+                        for (int k = 0; k < S; ++k)
+                            cd[k] = ((m >> k) & 1u) ? __hip_atomic_load(&dist[(int64_t)y * S + k], __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_WORKGROUP)
+                                                    : 0ull;
+                        uint32_t imp = 0, fimp = 0;
+#pragma unroll
+                        for (int k = 0; k < S; ++k) {
+                            if (!((m >> k) & 1u)) continue;
+                            ++relax;
+                            const double nd = dx[k] + we;
+                            if (!(nd <= wmax[k])) continue;
+                            const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
+                            if (nb >= cd[k]) continue;
+                            const unsigned long long old = atomicMin(&dist[(int64_t)y * S + k], nb);
+                            if (nb < old) {
+                                if (nd < s_thr[k]) {
+                                    imp |= 1u << k;
+                                } else {
+                                    fimp |= 1u << (kQMaskFarShift + k);
+                                    atomicMin(&s_farmin[k], nb);
+                                }
+                            }
+                        }
+                        if (imp | fimp) {
+                            const uint32_t add = fimp ? (imp | fimp | kQMaskFarListed | kQMaskTouched) : imp;
+                            const uint32_t om = atomicOr(&qmask[y], add);
+                            if (imp && (om & kQMaskSources) == 0) nxt[atomicAdd(&s_ncount, 1)] = y;
+                            if (fimp && !(om & kQMaskFarListed)) farA[atomicAdd(&s_nfar, 1)] = y;
+                            if (fimp && !(om & kQMaskTouched)) touched[atomicAdd(&s_tcount, 1)] = y;
+                            nearacc |= imp;
+                        }
+                    }
+                }
+            }
+            if (delta > 0.0) {  // which sources queued anything near this round
+                uint32_t v = nearacc;
+                for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off, 64);
+                if (lane == 0 && v) atomicOr(&s_nearany, v);
+                nearacc = 0;
             }
             __syncthreads();
             if (threadIdx.x == 0) {
@@ -646,6 +762,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                 }
                 bb_block_max_s<S>(mx, s_wkey);
             }
+            __shared__ uint32_t s_refill;
+            __shared__ double s_throld[S];
             if (threadIdx.x == 0) {
                 bool any = false;
                 for (int k = 0; k < S; ++k) {
@@ -653,8 +771,66 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                     any = any || s_wkey[k] != 0ull;
                 }
                 if (!any) s_fcount = 0;
+                // near-far: a source with nothing near queued and far labels pending
+                // moves its threshold past the least of them
+                uint32_t R = 0;
+                if (any && delta > 0.0)
+                    for (int k = 0; k < S; ++k)
+                        if (!((s_nearany >> k) & 1u) && s_farmin[k] != kInfBits) {
+                            R |= 1u << k;
+                            s_throld[k] = s_thr[k];
+                            const double m = __longlong_as_double((long long)s_farmin[k]);
+                            s_thr[k] = (m > s_thr[k] ? m : s_thr[k]) + delta;
+                            s_farmin[k] = kInfBits;
+                        }
+                s_refill = R;
+                s_nearany = 0;
+                s_nfar2 = 0;
+                s_farleft = any && s_nfar > 0 && (R || s_fcount > 0);
             }
             __syncthreads();
+            const uint32_t R = s_refill;
+            if (R) {
+                // far labels of the refilled sources: below the old threshold (expanded when
+                // they improved) or beyond the bound -> dropped; below the new one -> the
+                // frontier; the rest stay, and give the source's next least far label
+                const int nf = s_nfar;
+                for (int i = threadIdx.x; i < nf; i += NT) {
+                    const int32_t y = farA[i];
+                    const uint32_t om = __hip_atomic_load(&qmask[y], __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                    uint32_t clear = 0, set = 0;
+#pragma unroll
+                    for (int k = 0; k < S; ++k) {
+                        if (!((R >> k) & 1u) || !((om >> (kQMaskFarShift + k)) & 1u)) continue;
+                        const unsigned long long db = __hip_atomic_load(
+                            &dist[(int64_t)y * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        const double d = __longlong_as_double((long long)db);
+                        if (!(d <= s_wmax[k]) || d < s_throld[k]) {
+                            clear |= 1u << (kQMaskFarShift + k);
+                        } else if (d < s_thr[k]) {
+                            clear |= 1u << (kQMaskFarShift + k);
+                            set |= 1u << k;
+                        } else {
+                            atomicMin(&s_farmin[k], db);
+                        }
+                    }
+                    uint32_t nm = (om & ~clear) | set;
+                    if (!(nm & (kQMaskSources << kQMaskFarShift))) nm &= ~kQMaskFarListed;
+                    __hip_atomic_store(&qmask[y], nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (set && !(om & kQMaskSources)) cur[atomicAdd(&s_fcount, 1)] = y;
+                    if (nm & kQMaskFarListed) farB[atomicAdd(&s_nfar2, 1)] = y;
+                }
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    s_nfar = s_nfar2;
+                    s_farleft = s_nfar2 > 0;
+                }
+                int32_t *t = farA;
+                farA = farB;
+                farB = t;
+                __syncthreads();
+            }
         }
         // classify each source's unresolved targets
         for (int k = 0; k < S; ++k) {
@@ -938,7 +1114,8 @@ __global__ void k_bb_map(const int64_t *__restrict__ perm, const int64_t *__rest
 // misc + 4 as the bad-input flag.
 static void bb_build_graph(gs_ctx *c, int64_t n, int64_t E, const int64_t *dsrc, const int64_t *ddst,
                            const int64_t *osrc, const int64_t *odst, const double *dw,
-                           unsigned long long *misc, int64_t *&gp, int32_t *&gi, double *&gw) {
+                           unsigned long long *misc, int64_t *&gp, int32_t *&gi, double *&gw,
+                           double *wmed = nullptr) {
     hipStream_t s = c->stream;
     int *bad = (int *)(misc + 4);
     uint64_t *keys = (uint64_t *)c->buf("bb_keys").ensure(8 * E);
@@ -959,6 +1136,17 @@ static void bb_build_graph(gs_ctx *c, int64_t n, int64_t E, const int64_t *dsrc,
     GS_HIP(hipMemcpyAsync(&ucnt, misc, 8, hipMemcpyDeviceToHost, s));
     GS_HIP(hipStreamSynchronize(s));
     int64_t cnt2 = 2 * (int64_t)ucnt;
+    if (wmed) {  // median of <= 1023 evenly spaced unique-edge weights
+        *wmed = 0.0;
+        if (ucnt) {
+            const int64_t m = ucnt < 1023 ? (int64_t)ucnt : 1023, stride = (int64_t)ucnt / m;
+            std::vector<double> smp(m);
+            GS_HIP(hipMemcpy2DAsync(smp.data(), 8, uw, 8 * stride, 8, m, hipMemcpyDeviceToHost, s));
+            GS_HIP(hipStreamSynchronize(s));
+            std::nth_element(smp.begin(), smp.begin() + m / 2, smp.end());
+            *wmed = smp[m / 2];
+        }
+    }
     // G as symmetric CSR sorted by (row, col): unique keys -> no ties in order
     int64_t *pay = (int64_t *)c->buf("bb_pay").ensure(8 * (cnt2 + 1));
     k_bb_sym_payload<<<grid_for(cnt2 + 1, 256, 8192), 256, 0, s>>>(cnt2, pay);
@@ -1054,7 +1242,8 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
             int64_t *gp;
             int32_t *gi;
             double *gw;
-            bb_build_graph(c, n, E, dsrc, ddst, osrc, odst, dw, misc, gp, gi, gw);
+            double wmed = 0.0;
+            bb_build_graph(c, n, E, dsrc, ddst, osrc, odst, dw, misc, gp, gi, gw, &wmed);
             unsigned long long *deg = (unsigned long long *)b_flag.ensure(8 * (n + 1));
             // columns grouped by source row (stable: radix sort is stable)
             uint64_t *okeys = (uint64_t *)b_okeys.ensure(8 * E);
@@ -1155,7 +1344,7 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                 const int64_t nunits = (nsrc + S - 1) / S;
                 int64_t slabs = nunits < maxslabs ? nunits : maxslabs;
                 // keep the per-slab working set under ~8 GB
-                const double per = S == 1 ? 24.0 : 8.0 * S + 20.0;
+                const double per = S == 1 ? 24.0 : 8.0 * S + 28.0;
                 int64_t cap = (int64_t)(8e9 / (per * (double)(n ? n : 1)));
                 if (cap < 1) cap = 1;
                 if (slabs > cap) slabs = cap;
@@ -1176,11 +1365,18 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                                                        touched, misc + 1);
                 } else {
                     uint32_t *fm = (uint32_t *)c->buf("bb_fmask").ensure(4 * slabs * n);
+                    int32_t *farl = (int32_t *)c->buf("bb_far").ensure(8 * slabs * n);
                     auto *qm = (uint32_t *)qflag;
+                    // near-far step: half the median edge weight (GSPARSE_BB_NEARFAR = the
+                    // factor, 0 = plain frontier order)
+                    double nfs = 0.5;
+                    if (const char *e = getenv("GSPARSE_BB_NEARFAR")) nfs = atof(e);
+                    const double delta = nfs > 0.0 && wmed > 0.0 ? nfs * wmed : 0.0;
 #define GS_BBM(NT_, S_)                                                                        \
     k_bb_sssp_multi<NT_, S_><<<(unsigned)slabs, NT_, 0, s>>>(gp, gi, gw, n, sources, nsrc, optr, \
                                                             order, ddst, dw, eps, state, dist,  \
-                                                            qm, fr, fm, touched, misc + 1)
+                                                            qm, fr, fm, touched, farl, delta, \
+                                                            misc + 1)
                     if (bt == 1024) {
                         if (S == 2) GS_BBM(1024, 2); else if (S == 4) GS_BBM(1024, 4); else GS_BBM(1024, 8);
                     } else if (bt == 512) {

@@ -391,28 +391,41 @@ struct JacBitProbe {
 
 // Probe phase shared by the LDS-table and bitmap kernels (after jac_stage and
 // a barrier).  The d_u of the owner and each entry's d_v give the union.
-template <class Probe, int kJacUnroll = kJacUnrollDef>
+// UL list elements per lane are loaded at once (the global reads are what the
+// loop waits on), then probed UP at a time (the probe state is what costs
+// registers); GS_JAC_SKIP: 64-element steps past the list's end are skipped as a
+// whole (wave-uniform) instead of run with every lane masked off.
+#ifndef GS_JAC_SKIP
+#define GS_JAC_SKIP 0
+#endif
+template <class Probe, int UL = kJacUnrollDef, int UP = UL>
 __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix, int64_t du,
                                                  int64_t lo, const JacStage &st,
                                                  const JacSink &sk, const Probe &pr) {
+    static_assert(UL % UP == 0, "probe groups split the loaded elements");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     for (int k = wave; k < st.nbig; k += nw) {
-        const int64_t b = st.b[k], dv = st.dv[k];
+        const int64_t b = st.b[k];
+        const int32_t dv = __builtin_amdgcn_readfirstlane(st.dv[k]);
         int64_t cnt = 0;
-        for (int64_t j0 = 0; j0 < dv; j0 += 64 * kJacUnroll) {
-            int32_t xs[kJacUnroll];  // all loads in flight before the first probe
+        for (int32_t j0 = 0; j0 < dv; j0 += 64 * UL) {
+            int32_t xs[UL];  // all loads in flight before the first probe
 #pragma unroll
-            for (int t = 0; t < kJacUnroll; ++t) {
-                const int64_t j = j0 + t * 64 + lane;
+            for (int t = 0; t < UL; ++t) {
+                const int32_t j = j0 + t * 64 + lane;
                 xs[t] = j < dv ? ix[b + j] : -1;
             }
-            typename Probe::S ps[kJacUnroll];
 #pragma unroll
-            for (int t = 0; t < kJacUnroll; ++t) ps[t] = pr.first(xs[t] >= 0 ? xs[t] : 0);
+            for (int g = 0; g < UL; g += UP) {
+                if (GS_JAC_SKIP && j0 + g * 64 >= dv) break;
+                typename Probe::S ps[UP];
 #pragma unroll
-            for (int t = 0; t < kJacUnroll; ++t) {
-                const bool hit = xs[t] >= 0 && pr.done(xs[t], ps[t]);
-                cnt += __popcll(__ballot(hit));
+                for (int t = 0; t < UP; ++t) ps[t] = pr.first(xs[g + t] >= 0 ? xs[g + t] : 0);
+#pragma unroll
+                for (int t = 0; t < UP; ++t) {
+                    const bool hit = xs[g + t] >= 0 && pr.done(xs[g + t], ps[t]);
+                    cnt += __popcll(__ballot(hit));
+                }
             }
         }
         if (lane == 0) sk.put(lo + st.off[k], cnt, du, dv);
@@ -482,6 +495,149 @@ __global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ i
     __syncthreads();
     constexpr int U = C >= 16384 ? GS_JAC_UNROLL_BIG : kJacUnrollDef;
     jac_probe_staged<JacHashProbe, U>(ix, du, lo, st, sk, JacHashProbe{tab, shift, mask});
+}
+
+// Quotient tables (classes in GS_JAC_Q16, when the ids fit): 16-bit slots, so the
+// same LDS holds twice the slots -- half the load factor, and the 32K-slot class
+// runs two workgroups per CU instead of one.  h = (x * kJacMul) mod 2^b is a
+// bijection of [0, 2^b) (odd multiplier, n <= 2^b); its top bits pick the home
+// bucket, the low qb bits (the remainder) go into the slot with the bucket's
+// distance from home: slot = (d + 1) << qb | rem, 0 = empty.  (bucket, slot)
+// gives h back, so a match is exact.  Buckets of 8 slots (one 16-B LDS read per
+// probe step) fill from slot 0 up; a free slot 7 ends an unsuccessful search.
+// An insert that would go past the largest distance a slot can encode flags the
+// task, which then probes the owner's sorted list instead (never seen in practice).
+#ifndef GS_JAC_Q16
+#define GS_JAC_Q16 0xE  // classes 1, 2, 3
+#endif
+#ifndef GS_JAC_UNROLL_Q8  // the two-workgroups-per-CU 32K class: 64 VGPRs
+#define GS_JAC_UNROLL_Q8 4
+#endif
+#ifndef GS_JAC_LOADS_Q8  // ... with this many list loads per lane in flight
+#define GS_JAC_LOADS_Q8 8
+#endif
+static constexpr uint32_t kJacMul = 2654435761u;
+
+// any zero 16-bit half in v
+__device__ __forceinline__ uint32_t jac_hz16(uint32_t v) {
+    return (v - 0x00010001u) & ~v & 0x80008000u;
+}
+
+struct JacQParams {
+    uint32_t hmask, qb, rmask, dmax;  // 2^b - 1, remainder bits, 2^qb - 1, largest distance
+};
+
+struct JacQProbe {
+    const uint4 *tab;
+    JacQParams p;
+    uint32_t nbm;  // buckets - 1
+    struct S {
+        uint4 q;
+        uint32_t h;
+    };
+    __device__ __forceinline__ S first(int32_t x) const {
+        const uint32_t h = ((uint32_t)x * kJacMul) & p.hmask;
+        return S{tab[h >> p.qb], h};
+    }
+    __device__ __forceinline__ bool done(int32_t, S s) const {
+        const uint32_t home = s.h >> p.qb, rem = s.h & p.rmask;
+        for (uint32_t d = 0;;) {
+            const uint32_t t = ((d + 1) << p.qb) | rem, t2 = t | (t << 16);
+            if (jac_hz16(s.q.x ^ t2) | jac_hz16(s.q.y ^ t2) | jac_hz16(s.q.z ^ t2) |
+                jac_hz16(s.q.w ^ t2))
+                return true;
+            if ((s.q.w >> 16) == 0 || ++d > p.dmax) return false;
+            s.q = tab[(home + d) & nbm];
+        }
+    }
+};
+
+// the overflow path: binary search of the owner's sorted neighbour list
+struct JacSortedProbe {
+    const int32_t *row;
+    int64_t du;
+    struct S {};
+    __device__ __forceinline__ S first(int32_t) const { return S{}; }
+    __device__ __forceinline__ bool done(int32_t x, S) const {
+        int64_t lo = 0, hi = du;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (row[mid] < x) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo < du && row[lo] == x;
+    }
+};
+
+// one task per workgroup; C 16-bit slots in LDS; MINW waves per SIMD
+template <int C, int NT, int MINW>
+__global__ void __launch_bounds__(NT, MINW) k_jac_hashq(const int64_t *__restrict__ ip,
+                                                        const int32_t *__restrict__ ix,
+                                                        const int32_t *__restrict__ ntask,
+                                                        const int32_t *__restrict__ trow,
+                                                        const int32_t *__restrict__ ti, int64_t t0,
+                                                        JacQParams qp, JacSink sk) {
+    constexpr int NB = C / 8;
+    __shared__ uint4 tab[NB];
+    __shared__ JacStage st;
+    __shared__ int ovf;
+    const int64_t t = t0 + blockIdx.x;
+    const int32_t u = trow[t];
+    int64_t a, du, lo, hi;
+    jac_task_range(ip, ntask, u, ti[t], a, du, lo, hi);
+    if (threadIdx.x == 0) st.nbig = st.nsmall = ovf = 0;
+    for (int s = threadIdx.x; s < NB; s += blockDim.x) tab[s] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    jac_stage(ip, ix, u, du, lo, hi, st);
+    uint32_t *words = reinterpret_cast<uint32_t *>(tab);
+    for (int64_t e = a + threadIdx.x; e < a + du; e += blockDim.x) {
+        const uint32_t h = ((uint32_t)ix[e] * kJacMul) & qp.hmask;
+        const uint32_t home = h >> qp.qb, rem = h & qp.rmask;
+        bool in = false;
+        for (uint32_t d = 0; d <= qp.dmax && !in; ++d) {
+            const uint32_t ent = ((d + 1) << qp.qb) | rem;
+            uint32_t *w = words + ((home + d) & (NB - 1)) * 4;
+            for (int q = 0; q < 8 && !in; ++q) {
+                const int sh = (q & 1) * 16;
+                uint32_t cur = 0;  // guess: the word is empty
+                while (true) {
+                    if ((cur >> sh) & 0xFFFFu) break;  // slot taken: the next one
+                    const uint32_t prev = atomicCAS(&w[q >> 1], cur, cur | (ent << sh));
+                    if (prev == cur) {
+                        in = true;
+                        break;
+                    }
+                    cur = prev;
+                }
+            }
+        }
+        if (!in) ovf = 1;
+    }
+    __syncthreads();
+    if (ovf)
+        jac_probe_staged<JacSortedProbe, 1>(ix, du, lo, st, sk, JacSortedProbe{ix + a, du});
+    else
+        jac_probe_staged<JacQProbe, (MINW >= 8 ? GS_JAC_LOADS_Q8 : GS_JAC_UNROLL_BIG),
+                         (MINW >= 8 ? GS_JAC_UNROLL_Q8 : GS_JAC_UNROLL_BIG)>(ix, du, lo, st, sk,
+                                                                             JacQProbe{tab, qp, NB - 1});
+}
+
+// quotient-table parameters for C 16-bit slots and ids < n; false when the
+// remainder leaves too few distance bits (n past ~2^24)
+static bool jac_qparams(int64_t n, int C, JacQParams &p) {
+    int b = 1;
+    while (b < 31 && ((int64_t)1 << b) < n) ++b;
+    const int bb = __builtin_ctz((unsigned)(C / 8));
+    if (b < bb) b = bb;
+    const int qb = b - bb;
+    if (16 - qb < 4) return false;
+    p.hmask = b >= 32 ? 0xFFFFFFFFu : (uint32_t)(((uint64_t)1 << b) - 1);
+    p.qb = (uint32_t)qb;
+    p.rmask = (1u << qb) - 1;
+    uint32_t dmax = (1u << (16 - qb)) - 2;
+    if (dmax > (uint32_t)(C / 8 - 1)) dmax = (uint32_t)(C / 8 - 1);
+    p.dmax = dmax;
+    return true;
 }
 
 __global__ void k_jac_bitmap_build(const int64_t *__restrict__ ip, const int32_t *__restrict__ ix,
@@ -705,8 +861,18 @@ void jaccard_symmetric(gs_ctx *c, double *out, int part, int nparts, int counts,
             hs = c->aux[k];
             launched |= 1 << k;
         }
+        JacQParams qp{};
+        const bool q16 = k >= 1 && k <= 3 && ((GS_JAC_Q16 >> k) & 1) &&
+                         jac_qparams(n, k == 1 ? 16384 : 32768, qp);
+        // test hook: a smaller largest distance, so the overflow path runs
+        if (const char *e = q16 ? getenv("GSPARSE_JAC_QDMAX") : nullptr)
+            if (atoi(e) >= 0 && (uint32_t)atoi(e) < qp.dmax) qp.dmax = (uint32_t)atoi(e);
         if (k == 0) {
             k_jac_hash<2048><<<nb, 256, 0, hs>>>(ip, ix, ntask, trow, ti, tlo, sk);
+        } else if (q16 && k == 1) {
+            k_jac_hashq<16384, 512, 4><<<nb, 512, 0, hs>>>(ip, ix, ntask, trow, ti, tlo, qp, sk);
+        } else if (q16) {
+            k_jac_hashq<32768, 1024, 8><<<nb, 1024, 0, hs>>>(ip, ix, ntask, trow, ti, tlo, qp, sk);
         } else if (k == 1) {
             k_jac_hash<8192><<<nb, 512, 0, hs>>>(ip, ix, ntask, trow, ti, tlo, sk);
         } else if (k == 2) {

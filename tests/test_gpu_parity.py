@@ -367,6 +367,43 @@ def test_jaccard_owner_hash_classes_vs_oracle(gs, monkeypatch):
     assert bits_equal(e.jaccard(), ref)
 
 
+@pytest.mark.parametrize("qdmax", [None, "0", "1"])
+@pytest.mark.parametrize("graph", ["hub60k", "spread3m"])
+def test_jaccard_quotient_tables_vs_oracle(gs, monkeypatch, graph, qdmax):
+    """The 16-bit quotient tables of row classes 1-3 (gs_jaccard.hip k_jac_hashq):
+    hubs in every class, ids of 16 bits (hub60k) and of 22 bits (spread3m: the
+    remainder width of RMAT-22), and -- GSPARSE_JAC_QDMAX -- the largest encodable
+    bucket distance cut to 0 / 1, so tasks overflow and probe the sorted list."""
+    rng = np.random.default_rng(5)
+    if graph == "hub60k":
+        ei, n = _hub_graph()
+        extra = np.stack([np.full(6000, 6), np.arange(40000, 46000)])
+    else:
+        n = 3_000_000
+        ei = np.zeros((2, 0), dtype=np.int64)
+        extra = np.zeros((2, 0), dtype=np.int64)
+    hubs = []
+    for hub, cnt in [(11, 2500), (12, 4000), (13, 7000), (14, 12000), (15, 15000)]:
+        lv = rng.choice(min(n, 200000) if graph == "hub60k" else n, cnt, replace=False)
+        hubs.append(np.stack([np.full(cnt, hub), lv]))
+    # shared leaves between hubs, so intersections are non-trivial
+    shared = rng.choice(n, 3000, replace=False)
+    for hub in (12, 13, 14):
+        hubs.append(np.stack([np.full(3000, hub), shared]))
+    e2 = np.concatenate([ei, extra] + [h % n for h in hubs], axis=1)
+    e2 = np.concatenate([e2, e2[::-1]], axis=1)
+    ip, ix, _ = O.canonical_csr(e2, n)
+    deg = np.diff(ip)
+    for lo, hi in [(1024, 4096), (4096, 8192), (8192, 16384)]:
+        assert ((deg > lo) & (deg <= hi)).any(), (lo, hi)
+    ref = O.jaccard(ip, ix)
+    if qdmax is not None:
+        monkeypatch.setenv("GSPARSE_JAC_QDMAX", qdmax)
+    data = gs.Data(edge_index=torch.from_numpy(e2), num_nodes=n)
+    e = gs.GraphSparsifier(data, "cpu")._engine
+    assert bits_equal(e.jaccard(), ref)
+
+
 @pytest.mark.parametrize("nparts", [1, 2, 3, 8])
 def test_jaccard_parts_sum_to_whole(gs, nparts):
     ei, n = _hub_graph()
@@ -862,4 +899,31 @@ def test_backbone_multi_source_searches(gs, S, threads, monkeypatch):
         monkeypatch.setenv("GSPARSE_BB_MULTI", "1")
         single = backbone_mask(ei, n, w)
         monkeypatch.setenv("GSPARSE_BB_MULTI", S)
+        assert np.array_equal(multi, single)
+
+
+@pytest.mark.parametrize("nearfar", ["0", "0.02", "0.5", "6"])
+def test_backbone_near_far_order(gs, nearfar, monkeypatch):
+    """k_bb_sssp_multi's near-far order (GSPARSE_BB_NEARFAR = the step as a
+    multiple of the median edge weight; 0 = plain frontier order): tiny steps
+    (many threshold moves, far piles refilled and compacted often), the default,
+    and steps past most distances -- the RMAT-12 oracle's keep mask, and the
+    single-source searches' on RMAT-14 / the hub graph with the certificates off."""
+    from gsparse import graphs
+    from gsparse.metric_backbone import backbone_mask
+
+    monkeypatch.setenv("GSPARSE_BB_NEARFAR", nearfar)
+    monkeypatch.setenv("GSPARSE_BB_MULTI", "8")
+    monkeypatch.setenv("GSPARSE_BB_THREADS", "1024")
+    ei, n = graphs.rmat(12, 8, seed=2), 1 << 12
+    ip, ix, _ = O.canonical_csr(ei, n)
+    cost = O.scores_to_cost(O.jaccard(ip, ix), "jaccard")
+    assert np.array_equal(backbone_mask(ei, n, cost[: ei.shape[1]]), O.metric_backbone(ei, n, cost))
+    monkeypatch.setenv("GSPARSE_BB_LANDMARKS", "0")
+    for ei, n in [(graphs.rmat(14, 8, seed=3), 1 << 14), _hub_graph()]:
+        w = _column_costs(ei, n)
+        multi = backbone_mask(ei, n, w)
+        monkeypatch.setenv("GSPARSE_BB_MULTI", "1")
+        single = backbone_mask(ei, n, w)
+        monkeypatch.setenv("GSPARSE_BB_MULTI", "8")
         assert np.array_equal(multi, single)

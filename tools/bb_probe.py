@@ -8,7 +8,7 @@ rows are its own) -- and timed with HIP events (the library's profiler).  The
 parts' keep bytes must add up to the whole mask.  Prints one JSON line: per N
 every part's time, the slowest, and its ratio to the mean.
 
-usage: bb_probe.py [SCALE] [REPS]"""
+usage: bb_probe.py [SCALE] [REPS] [whole]   (whole: the one-part run only)"""
 import ctypes
 import json
 import os
@@ -26,6 +26,7 @@ from gsparse.engine import Engine  # noqa: E402
 
 scale = int(sys.argv[1]) if len(sys.argv) > 1 else 18
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+whole_only = len(sys.argv) > 3 and sys.argv[3] == "whole"
 t = time.perf_counter()
 ei = graphs.rmat(scale, 8, seed=0)
 n = 1 << scale
@@ -73,8 +74,9 @@ run(0, 1, whole)  # warm-up
 out = {"workload": f"RMAT-{scale} metric backbone, one rank's work per part", "E": E,
        "graph_gen_s": round(gen, 2), "whole_ms": round(timed(lambda: run(0, 1, whole)), 2),
        "kept": int(whole.sum().item()), "whole_phases_ms": dict(phase_ms), "per_n": {}}
-print(json.dumps({"whole_ms": out["whole_ms"]}), flush=True)
-for N in (2, 4, 8):
+print(json.dumps({"whole_ms": out["whole_ms"], "relaxations": relax.value,
+                  "near_far": os.environ.get("GSPARSE_BB_NEARFAR", "default")}), flush=True)
+for N in (() if whole_only else (2, 4, 8)):
     parts, rel, phases = [], [], []
     tot = torch.zeros(E, dtype=torch.int32, device=dev)
     for r in range(N):
