@@ -459,7 +459,12 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     unsigned long long *__restrict__ dist_all, uint32_t *__restrict__ qmask_all,
     int32_t *__restrict__ fr_all, uint32_t *__restrict__ fm_all, int32_t *__restrict__ touched_all,
     int32_t *__restrict__ far_all, double delta, unsigned long long *__restrict__ relax_total) {
-    static_assert(S >= 1 && S <= 8, "1..8 sources per workgroup");
+    static_assert(S >= 1 && S <= 16, "1..16 sources per workgroup");
+    // queue bits of the per-node mask; the near-far order needs S more bits for the
+    // far pile (S <= 8 only: 16 sources fill the word)
+    constexpr uint32_t QS = S <= 8 ? kQMaskSources : 0xffffu;
+    constexpr bool NF = S <= 8;
+    if (!NF) delta = 0.0;
     constexpr int NW = NT / 64;
     __shared__ int s_fcount, s_ncount, s_tcount, s_nfar, s_nfar2, s_farleft, s_nheavy;
     __shared__ int32_t s_heavy[kBbHeavyMax];
@@ -540,9 +545,15 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
         while (true) {
             const int fc = s_fcount;
             if (fc == 0 && !s_farleft) break;
-            double wmax[S];
+            // the bounds in registers (8 sources or fewer), else read from LDS per relaxation
+            constexpr int SW = S <= 8 ? S : 1;
+            double wmax[SW];
 #pragma unroll
-            for (int k = 0; k < S; ++k) wmax[k] = s_wmax[k];
+            for (int k = 0; k < SW; ++k) wmax[k] = s_wmax[k];
+            auto wmax_of = [&](int k) -> double {
+                if constexpr (S <= 8) return wmax[k];
+                else return s_wmax[k];
+            };
             if (threadIdx.x == 0) s_nheavy = 0;
             __syncthreads();
             // heavy frontier nodes (more than kBbHeavy entries: the R-MAT hubs) are taken
@@ -550,7 +561,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
             // wave does not walk a hub's list while the others wait at the barrier
             for (int f = threadIdx.x; f < fc; f += NT) {
                 const int32_t x = cur[f];
-                uint32_t m = atomicAnd(&qmask[x], ~kQMaskSources) & kQMaskSources;
+                uint32_t m = atomicAnd(&qmask[x], ~QS) & QS;
                 if (m && gp[x + 1] - gp[x] > kBbHeavy) {
                     const int h = atomicAdd(&s_nheavy, 1);
                     if (h < kBbHeavyMax) {
@@ -590,7 +601,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                constexpr int U = S >= 8 ? 2 : 4;  // edges per lane per trip, all loads in flight
+                constexpr int U = S >= 16 ? 1 : S >= 8 ? 2 : 4;  // edges per lane per trip, all loads in flight
                 for (int e0 = 0; e0 < total; e0 += 64 * U) {
                     int lo[U];
                     uint32_t mm[U];
@@ -629,12 +640,12 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                         if (!((mm[u] >> k) & 1u)) continue;
                         ++relax;
                         const double nd = w_d[wv][lo[u]][k] + we[u];
-                        if (!(nd <= wmax[k])) continue;
+                        if (!(nd <= wmax_of(k))) continue;
                         const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
                         if (nb >= cd[u][k]) continue;
                         const unsigned long long old = atomicMin(&dist[(int64_t)y[u] * S + k], nb);
                         if (nb < old) {
-                            if (nd < s_thr[k]) {  // LDS: read on improvements only
+                            if (!NF || nd < s_thr[k]) {  // LDS: read on improvements only
                                 imp |= 1u << k;
                             } else {
                                 fimp |= 1u << (kQMaskFarShift + k);
@@ -645,7 +656,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                     if (imp | fimp) {  // queue y once per round; far: list it once, reset list
                         const uint32_t add = fimp ? (imp | fimp | kQMaskFarListed | kQMaskTouched) : imp;
                         const uint32_t om = atomicOr(&qmask[y[u]], add);
-                        if (imp && (om & kQMaskSources) == 0) {
+                        if (imp && (om & QS) == 0) {
                             const int q = atomicAdd(&s_ncount, 1);
                             nxt[q] = y[u];
                         }
@@ -664,13 +675,14 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                 for (int h = 0; h < nh; ++h) {
                     const int32_t x = s_heavy[h];
                     const uint32_t m = s_hmask[h];
-                    double dx[S];
-#pragma unroll
-                    for (int k = 0; k < S; ++k)
-                        dx[k] = ((m >> k) & 1u) ? __longlong_as_double((long long)__hip_atomic_load(
-                                                      &dist[(int64_t)x * S + k], __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP))
-                                                : 0.0;
+                    // the hub's labels: wave 0 stages them in its w_d row 0 (free after the
+                    // light chunks), every wave reads them from there
+                    if (wv == 0 && lane < S)
+                        w_d[0][0][lane] = ((m >> lane) & 1u) ? __longlong_as_double((long long)__hip_atomic_load(
+                                                                   &dist[(int64_t)x * S + lane], __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_WORKGROUP))
+                                                             : 0.0;
+                    __syncthreads();
                     const int64_t e1 = gp[x + 1];
                     for (int64_t e = gp[x] + threadIdx.x; e < e1; e += NT) {
                         const int32_t y = gi[e];
@@ -686,13 +698,13 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                         for (int k = 0; k < S; ++k) {
                             if (!((m >> k) & 1u)) continue;
                             ++relax;
-                            const double nd = dx[k] + we;
-                            if (!(nd <= wmax[k])) continue;
+                            const double nd = w_d[0][0][k] + we;
+                            if (!(nd <= wmax_of(k))) continue;
                             const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
                             if (nb >= cd[k]) continue;
                             const unsigned long long old = atomicMin(&dist[(int64_t)y * S + k], nb);
                             if (nb < old) {
-                                if (nd < s_thr[k]) {
+                                if (!NF || nd < s_thr[k]) {
                                     imp |= 1u << k;
                                 } else {
                                     fimp |= 1u << (kQMaskFarShift + k);
@@ -703,15 +715,16 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                         if (imp | fimp) {
                             const uint32_t add = fimp ? (imp | fimp | kQMaskFarListed | kQMaskTouched) : imp;
                             const uint32_t om = atomicOr(&qmask[y], add);
-                            if (imp && (om & kQMaskSources) == 0) nxt[atomicAdd(&s_ncount, 1)] = y;
+                            if (imp && (om & QS) == 0) nxt[atomicAdd(&s_ncount, 1)] = y;
                             if (fimp && !(om & kQMaskFarListed)) farA[atomicAdd(&s_nfar, 1)] = y;
                             if (fimp && !(om & kQMaskTouched)) touched[atomicAdd(&s_tcount, 1)] = y;
                             nearacc |= imp;
                         }
                     }
+                    __syncthreads();
                 }
             }
-            if (delta > 0.0) {  // which sources queued anything near this round
+            if (NF && delta > 0.0) {  // which sources queued anything near this round
                 uint32_t v = nearacc;
                 for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off, 64);
                 if (lane == 0 && v) atomicOr(&s_nearany, v);
@@ -774,7 +787,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                 // near-far: a source with nothing near queued and far labels pending
                 // moves its threshold past the least of them
                 uint32_t R = 0;
-                if (any && delta > 0.0)
+                if (NF && any && delta > 0.0)
                     for (int k = 0; k < S; ++k)
                         if (!((s_nearany >> k) & 1u) && s_farmin[k] != kInfBits) {
                             R |= 1u << k;
@@ -789,8 +802,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                 s_farleft = any && s_nfar > 0 && (R || s_fcount > 0);
             }
             __syncthreads();
-            const uint32_t R = s_refill;
-            if (R) {
+            const uint32_t R = NF ? s_refill : 0u;
+            if (NF && R) {
                 // far labels of the refilled sources: below the old threshold (expanded when
                 // they improved) or beyond the bound -> dropped; below the new one -> the
                 // frontier; the rest stay, and give the source's next least far label
@@ -816,9 +829,9 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                         }
                     }
                     uint32_t nm = (om & ~clear) | set;
-                    if (!(nm & (kQMaskSources << kQMaskFarShift))) nm &= ~kQMaskFarListed;
+                    if (!(nm & (QS << kQMaskFarShift))) nm &= ~kQMaskFarListed;
                     __hip_atomic_store(&qmask[y], nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (set && !(om & kQMaskSources)) cur[atomicAdd(&s_fcount, 1)] = y;
+                    if (set && !(om & QS)) cur[atomicAdd(&s_fcount, 1)] = y;
                     if (nm & kQMaskFarListed) farB[atomicAdd(&s_nfar2, 1)] = y;
                 }
                 __syncthreads();
@@ -1336,16 +1349,16 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                 // sources searched together per workgroup (k_bb_sssp_multi), 1 = alone: 8 on
                 // large graphs (RMAT-18: 2.81 s vs 3.07 s alone; 4 sources 3.14 s), alone on
                 // small ones (Roman: 2.30 ms vs 2.45 ms with 8)
-                int S = big ? 8 : 1;
+                int S = big ? 16 : 1;
                 if (const char *e = getenv("GSPARSE_BB_MULTI")) {
                     const int v = atoi(e);
-                    S = v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
+                    S = v >= 16 ? 16 : v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
                 }
                 const int64_t nunits = (nsrc + S - 1) / S;
                 int64_t slabs = nunits < maxslabs ? nunits : maxslabs;
-                // keep the per-slab working set under ~8 GB
+                // keep the working set of all slabs under ~24 GB (of 288)
                 const double per = S == 1 ? 24.0 : 8.0 * S + 28.0;
-                int64_t cap = (int64_t)(8e9 / (per * (double)(n ? n : 1)));
+                int64_t cap = (int64_t)(24e9 / (per * (double)(n ? n : 1)));
                 if (cap < 1) cap = 1;
                 if (slabs > cap) slabs = cap;
                 unsigned long long *dist =
@@ -1378,11 +1391,14 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                                                             qm, fr, fm, touched, farl, delta, \
                                                             misc + 1)
                     if (bt == 1024) {
-                        if (S == 2) GS_BBM(1024, 2); else if (S == 4) GS_BBM(1024, 4); else GS_BBM(1024, 8);
+                        if (S == 2) GS_BBM(1024, 2); else if (S == 4) GS_BBM(1024, 4);
+                        else if (S == 8) GS_BBM(1024, 8); else GS_BBM(1024, 16);
                     } else if (bt == 512) {
-                        if (S == 2) GS_BBM(512, 2); else if (S == 4) GS_BBM(512, 4); else GS_BBM(512, 8);
+                        if (S == 2) GS_BBM(512, 2); else if (S == 4) GS_BBM(512, 4);
+                        else if (S == 8) GS_BBM(512, 8); else GS_BBM(512, 16);
                     } else {
-                        if (S == 2) GS_BBM(256, 2); else if (S == 4) GS_BBM(256, 4); else GS_BBM(256, 8);
+                        if (S == 2) GS_BBM(256, 2); else if (S == 4) GS_BBM(256, 4);
+                        else if (S == 8) GS_BBM(256, 8); else GS_BBM(256, 16);
                     }
 #undef GS_BBM
                 }

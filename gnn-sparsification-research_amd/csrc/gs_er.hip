@@ -1793,9 +1793,9 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
                  (long long)col1, (long long)er.proj_c0, (long long)er.proj_c1);
         GS_HIP(hipSetDevice(c->device));
         const int64_t n = er.n, k = er.k;
-        GS_CHECK(blas_threads <= kMaxChunks || n <= 10000, GS_EUNSUPPORTED,
-                 "blas_threads=%d: the OpenBLAS ddot order is reproduced for at most %d threads "
-                 "(NumPy's OpenBLAS is built with MAX_THREADS=64)", blas_threads, kMaxChunks);
+        // OpenBLAS caps its thread count at MAX_THREADS (64 in NumPy's build): a larger
+        // request runs -- and orders the ddot sums -- as 64 threads
+        if (blas_threads > kMaxChunks) blas_threads = kMaxChunks;
         ChunkArg ch = to_arg(make_chunks(n, blas_threads));
         // two columns per lane (16-B accesses) unless that leaves too few waves
         const int64_t ncols = col1 - col0;

@@ -71,6 +71,20 @@ def tree_sum(parts):
     return parts[0]
 
 
+def fold_pairwise(parts):
+    """tree_sum of a power-of-two number of parts, folded as they arrive: a stack of
+    at most log2(count) + 1 partial sums instead of every part at once."""
+    stack = []
+    for p in parts:
+        stack.append((1, p))
+        while len(stack) >= 2 and stack[-1][0] == stack[-2][0]:
+            (s, right), (_, left) = stack.pop(), stack.pop()
+            stack.append((2 * s, left + right))
+    if len(stack) != 1:
+        raise ValueError("fold_pairwise needs a power-of-two number of parts")
+    return stack[0][1]
+
+
 def finalize_er(total):
     """metrics.py:293-297 on the tree-combined sum (0 + s, nan_to_num, clamp)."""
     t = 0.0 + total
@@ -114,6 +128,12 @@ class Comm:
         out = [torch.empty_like(local, device=self.device) for _ in range(self.world)]
         dist.all_gather(out, local.to(self.device), group=self.group)
         return out
+
+    def broadcast_from(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        """Broadcast from group rank `src` (in place on the receivers)."""
+        g = src if self.group is None else dist.get_global_rank(self.group, src)
+        dist.broadcast(t, src=g, group=self.group)
+        return t
 
     def all_gather_flat(self, local: torch.Tensor) -> torch.Tensor:
         """Equal-size shards concatenated in rank order (one RCCL all-gather
@@ -293,26 +313,37 @@ def sharded_approx_er(engine, comm: Comm, epsilon: float = 0.3, seed: int = 42,
     else:
         engine.er_project_host(rng, k, cols=cols)
     covers = [dyadic_cover(a, b) for a, b in runs]
-    slots = max(1, max(len(cv) for cv in covers))
     cuda = comm.device.type == "cuda"
-    local = torch.zeros((slots, engine.nnz), dtype=torch.float64,
-                        device=comm.device if cuda else "cpu")
+    dev = comm.device if cuda else "cpu"
+    nnz = engine.nnz
+    local = torch.zeros((max(1, len(covers[comm.rank])), nnz), dtype=torch.float64, device=dev)
     if b > a:
         engine.er_solve(bounds[a], bounds[b], max_cg_iters, cg_tol, blas_threads)
         for i, (lev, idx) in enumerate(covers[comm.rank]):
             lo, hi = idx << lev, (idx + 1) << lev
-            # fold the block's 2**lev nodes in tree order (gs_er_scores per node)
-            parts = []
-            for f in range(lo, hi):
-                o = torch.empty(engine.nnz, dtype=torch.float64, device=comm.device) if cuda else None
-                p = engine.er_scores(bounds[f], bounds[f + 1], finalize=False, out=o)
-                parts.append(p if cuda else torch.from_numpy(np.asarray(p)))
-            local[i] = tree_sum(parts)
-    gathered = comm.all_gather_flat(local.reshape(-1)).reshape(comm.world, slots, engine.nnz)
+
+            def node_sums():  # the block's 2**lev nodes in tree order (gs_er_scores per node)
+                for f in range(lo, hi):
+                    o = torch.empty(nnz, dtype=torch.float64, device=comm.device) if cuda else None
+                    p = engine.er_scores(bounds[f], bounds[f + 1], finalize=False, out=o)
+                    yield p if cuda else torch.from_numpy(np.asarray(p))
+
+            local[i] = fold_pairwise(node_sums())
+    slots = [len(cv) for cv in covers]
+    if all(sl == 1 for sl in slots):  # power-of-two world: one node per rank, one all-gather
+        gathered = comm.all_gather_flat(local.reshape(-1)).reshape(comm.world, 1, nnz)
+        blocks = [gathered[r] for r in range(comm.world)]
+    else:  # every rank's real blocks only, from that rank
+        blocks = [local if r == comm.rank else torch.empty((max(1, slots[r]), nnz), dtype=torch.float64,
+                                                          device=dev)
+                  for r in range(comm.world)]
+        for r in range(comm.world):
+            if slots[r]:
+                comm.broadcast_from(blocks[r], r)
     level = {}
     for r, cv in enumerate(covers):
         for i, key in enumerate(cv):
-            level[key] = gathered[r, i]
+            level[key] = blocks[r][i]
     for lev in range(depth):  # combine siblings bottom-up: the pairwise tree's own order
         for idx in range((1 << depth) >> (lev + 1)):
             lk, rk = (lev, 2 * idx), (lev, 2 * idx + 1)

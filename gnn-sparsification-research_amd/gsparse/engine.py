@@ -27,7 +27,15 @@ def blas_threads_default() -> int:
     """OpenBLAS thread count NumPy would use for np.dot in this process.
 
     The reference's CG dot products are OpenBLAS ddot calls whose reduction
-    order depends on it (n > 10000); GSPARSE_BLAS_THREADS overrides."""
+    order depends on it (n > 10000); GSPARSE_BLAS_THREADS overrides.  Clamped to
+    OpenBLAS's MAX_THREADS (64 in NumPy's build), as OpenBLAS itself does."""
+    return min(_blas_threads_requested(), OPENBLAS_MAX_THREADS)
+
+
+OPENBLAS_MAX_THREADS = 64
+
+
+def _blas_threads_requested() -> int:
     env = os.environ.get("GSPARSE_BLAS_THREADS")
     if env:
         return max(1, int(env))

@@ -179,6 +179,14 @@ def test_tree_helpers():
     assert edge_ranges(10, 3) == [0, 3, 6, 10]
     assert pow2_floor(6) == 4 and pow2_floor(8) == 8 and pow2_floor(1) == 1
     assert tree_sum([1.0, 2.0, 3.0, 4.0]) == (1.0 + 2.0) + (3.0 + 4.0)
+    from gsparse.distributed import fold_pairwise
+
+    rng = np.random.default_rng(3)
+    for cnt in (1, 2, 4, 8, 16):
+        parts = [rng.standard_normal(5) * 10.0 ** rng.integers(-8, 8) for _ in range(cnt)]
+        assert np.array_equal(fold_pairwise(iter(parts)), tree_sum(parts))
+    with pytest.raises(ValueError):
+        fold_pairwise([1.0, 2.0, 3.0])
     assert dyadic_cover(0, 32) == [(5, 0)]
     assert dyadic_cover(5, 11) == [(0, 5), (1, 3), (1, 4), (0, 10)]
     assert dyadic_cover(3, 3) == []

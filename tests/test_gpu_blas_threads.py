@@ -55,11 +55,13 @@ def test_approx_er_high_blas_threads(gs, chunked_hi, threads, mode, monkeypatch)
     assert bits_equal(er, ref[threads])
 
 
-def test_more_than_64_blas_threads_refused(gs, chunked_hi):
-    n, ei, _ = chunked_hi
+def test_more_than_64_blas_threads_run_as_64(gs, chunked_hi):
+    """OpenBLAS caps its thread count at MAX_THREADS (64): a larger request orders the
+    ddot sums as 64 threads do -- here as in the library (gs_er_solve clamps)."""
+    n, ei, ref = chunked_hi
     sp_ = gs.GraphSparsifier(gs.Data(edge_index=torch.from_numpy(ei), num_nodes=n), "cpu")
-    with pytest.raises(NotImplementedError):
-        sp_._engine.approx_er(epsilon=0.9, max_cg_iters=5, blas_threads=65)
+    assert bits_equal(sp_._engine.approx_er(epsilon=0.9, max_cg_iters=60, blas_threads=65), ref[64])
+    assert bits_equal(sp_._engine.approx_er(epsilon=0.9, max_cg_iters=60, blas_threads=200), ref[64])
 
 
 @pytest.fixture(scope="module")

@@ -868,7 +868,7 @@ def test_geodesic_violations_vs_networkx(gs, name):
 
 
 @pytest.mark.parametrize("threads", ["256", "1024"])
-@pytest.mark.parametrize("S", ["2", "4", "8"])
+@pytest.mark.parametrize("S", ["2", "4", "8", "16"])
 def test_backbone_multi_source_searches(gs, S, threads, monkeypatch):
     """S sources per workgroup (GSPARSE_BB_MULTI, interleaved labels): the keep
     masks of the reference goldens, of the RMAT-12 oracle, and of the

@@ -174,6 +174,16 @@ def test_blas_threads_default_is_openblas_count():
             assert blas_threads_default() == t
 
 
+def test_blas_threads_default_clamped_to_openblas_max(monkeypatch):
+    """OpenBLAS runs at most MAX_THREADS (64) threads whatever is asked for."""
+    from gsparse.engine import blas_threads_default
+
+    monkeypatch.setenv("GSPARSE_BLAS_THREADS", "200")
+    assert blas_threads_default() == 64
+    monkeypatch.setenv("GSPARSE_BLAS_THREADS", "7")
+    assert blas_threads_default() == 7
+
+
 def test_bench_refuses_more_gpus_than_visible():
     """bench.py --gpus N starts N ranks itself, and fails loudly when fewer
     than N GPUs are visible (none here)."""
