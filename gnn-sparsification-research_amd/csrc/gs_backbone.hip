@@ -410,6 +410,22 @@ __global__ void __launch_bounds__(NT) k_bb_sssp(
     if (threadIdx.x == 0) atomicAdd(relax_total, s_relax);
 }
 
+// Lower a label whose prefetched value was above nb.  GS_BB_NORET: fire and forget
+// (the wave does not wait for the atomic's return), and y counts as improved on the
+// prefetched value alone -- when another lane got there first, y is queued for a
+// source whose label it did not lower, an extra expansion that changes no fixpoint.
+#ifndef GS_BB_NORET
+#define GS_BB_NORET 1
+#endif
+__device__ __forceinline__ bool bb_min_improves(unsigned long long *p, unsigned long long nb) {
+#if GS_BB_NORET
+    atomicMin(p, nb);
+    return true;
+#else
+    return nb < atomicMin(p, nb);
+#endif
+}
+
 // order-preserving u64 key of a double (0 below every key: "no value")
 __device__ __forceinline__ unsigned long long dkey(double v) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -643,8 +659,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                         if (!(nd <= wmax_of(k))) continue;
                         const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
                         if (nb >= cd[u][k]) continue;
-                        const unsigned long long old = atomicMin(&dist[(int64_t)y[u] * S + k], nb);
-                        if (nb < old) {
+                        if (bb_min_improves(&dist[(int64_t)y[u] * S + k], nb)) {
                             if (!NF || nd < s_thr[k]) {  // LDS: read on improvements only
                                 imp |= 1u << k;
                             } else {
@@ -702,8 +717,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                             if (!(nd <= wmax_of(k))) continue;
                             const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
                             if (nb >= cd[k]) continue;
-                            const unsigned long long old = atomicMin(&dist[(int64_t)y * S + k], nb);
-                            if (nb < old) {
+                            if (bb_min_improves(&dist[(int64_t)y * S + k], nb)) {
                                 if (!NF || nd < s_thr[k]) {
                                     imp |= 1u << k;
                                 } else {
@@ -1356,9 +1370,9 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                 }
                 const int64_t nunits = (nsrc + S - 1) / S;
                 int64_t slabs = nunits < maxslabs ? nunits : maxslabs;
-                // keep the working set of all slabs under ~24 GB (of 288)
+                // keep the working set of all slabs under ~48 GB (of 288)
                 const double per = S == 1 ? 24.0 : 8.0 * S + 28.0;
-                int64_t cap = (int64_t)(24e9 / (per * (double)(n ? n : 1)));
+                int64_t cap = (int64_t)(48e9 / (per * (double)(n ? n : 1)));
                 if (cap < 1) cap = 1;
                 if (slabs > cap) slabs = cap;
                 unsigned long long *dist =
