@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 namespace gs {
@@ -426,6 +427,104 @@ __device__ __forceinline__ bool bb_min_improves(unsigned long long *p, unsigned 
 #endif
 }
 
+// Reverse columns (metric_backbone.py:97-111 decides column (v, u) from v's Dijkstra,
+// column (u, v) from u's).  After u's search, D = u's label of v (the left fold of a
+// real u-v path; m bounds the relative rounding of folds over simple paths, as in
+// k_bb_certify):
+//  * prune: d_fl(v, u) <= D (1 + m) (the same path folded from v), so a reverse
+//    column with w > (D (1 + m) + eps)(1 + m) is pruned;
+//  * exact: when u's search ran dry within bound bk >= D (frontier empty), labels
+//    <= bk are exact and every other label exceeds bk, so A = min over v's other G
+//    neighbours x of (label(x), or bk if beyond it) + w(x, v) bounds every u-v path
+//    but the edge itself from below: real length >= A (1 - m).  A (1 - 3m) > D then
+//    means the edge is the only shortest path from either end by more than any
+//    rounding, so d_fl(v, u) = fl(0 + w_G) = D exactly, and the reverse column is
+//    decided as the reference decides it: w <= D + eps.  (v of more than kBbCrossDeg
+//    neighbours is left to its own search.)
+//  * keep, v unreached: d_fl(u, v) > bk, so w <= (bk (1 - m) + eps)(1 - m) keeps it.
+// Whatever falls within the margins stays open for v's own search.
+// skeys / sidx: every column's (row * n + col) key in ascending order and its column;
+// rp: the first position of the reverse key (-1: none).
+#ifndef GS_BB_CROSS_DEG
+#define GS_BB_CROSS_DEG 512
+#endif
+static constexpr int64_t kBbCrossDeg = GS_BB_CROSS_DEG;
+template <int S>
+__device__ __forceinline__ void bb_cross_decide(const uint64_t *__restrict__ skeys,
+                                                const int64_t *__restrict__ sidx, int64_t rp,
+                                                int64_t u, int64_t v, int64_t n, int64_t E,
+                                                int k, unsigned long long db, double bk, double m,
+                                                double eps, const double *__restrict__ w,
+                                                const int64_t *__restrict__ gp,
+                                                const int32_t *__restrict__ gi,
+                                                const double *__restrict__ gw,
+                                                const unsigned long long *__restrict__ dist,
+                                                uint8_t *__restrict__ state) {
+    if (rp < 0) return;
+    const uint64_t rkey = (uint64_t)v * (uint64_t)n + (uint64_t)u;
+    bool open = false;  // any reverse column still undecided
+    for (int64_t p = rp; p < E && skeys[p] == rkey; ++p) open = open || state[sidx[p]] == 0;
+    if (!open) return;
+    const bool reached = db != kInfBits;
+    const double D = __longlong_as_double((long long)db);
+    bool exact = false;
+    if (reached && bk >= 0.0 && D <= bk && gp[v + 1] - gp[v] <= kBbCrossDeg) {
+        double A = __longlong_as_double((long long)kInfBits);
+        for (int64_t e = gp[v]; e < gp[v + 1]; ++e) {
+            const int32_t x = gi[e];
+            if (x == u) continue;
+            const unsigned long long bx = __hip_atomic_load(&dist[(int64_t)x * S + k], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+            const double dx = __longlong_as_double((long long)bx);
+            const double lb = (bx != kInfBits && dx <= bk) ? dx : bk;
+            const double a = lb + gw[e];
+            A = a < A ? a : A;
+        }
+        exact = A * (1.0 - 3.0 * m) > D;
+    }
+    const double hi = reached ? (D * (1.0 + m) + eps) * (1.0 + m) : 0.0;
+    const bool keep_unreached = !reached && bk >= 0.0;
+    const double lo = keep_unreached ? (bk * (1.0 - m) + eps) * (1.0 - m) : -1.0;
+    for (int64_t p = rp; p < E && skeys[p] == rkey; ++p) {
+        const int64_t r = sidx[p];
+        if (state[r] != 0) continue;
+        const double wr = w[r];
+        if (exact) state[r] = wr <= D + eps ? 1 : 2;
+        else if (reached && wr > hi) state[r] = 2;
+        else if (keep_unreached && wr <= lo) state[r] = 1;
+    }
+}
+
+// (row * n + col) key of every column, for the reverse-column lookup
+__global__ void k_bb_pairkeys(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
+                              int64_t E, int64_t n, uint64_t *__restrict__ keys,
+                              int64_t *__restrict__ idx) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        keys[i] = (uint64_t)src[i] * (uint64_t)n + (uint64_t)dst[i];
+        idx[i] = i;
+    }
+}
+
+// first position of column i's reverse key (col * n + row) in the sorted keys, -1 if
+// absent or a self-loop
+__global__ void k_bb_revpos(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
+                            int64_t E, int64_t n, const uint64_t *__restrict__ skeys,
+                            int64_t *__restrict__ rpos) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t u = src[i], v = dst[i];
+        const uint64_t key = (uint64_t)v * (uint64_t)n + (uint64_t)u;
+        int64_t lo = 0, hi = E;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (skeys[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        rpos[i] = (u != v && lo < E && skeys[lo] == key) ? lo : -1;
+    }
+}
+
 // order-preserving u64 key of a double (0 below every key: "no value")
 __device__ __forceinline__ unsigned long long dkey(double v) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -474,7 +573,9 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     const double *__restrict__ w, double eps, uint8_t *__restrict__ state,
     unsigned long long *__restrict__ dist_all, uint32_t *__restrict__ qmask_all,
     int32_t *__restrict__ fr_all, uint32_t *__restrict__ fm_all, int32_t *__restrict__ touched_all,
-    int32_t *__restrict__ far_all, double delta, unsigned long long *__restrict__ relax_total) {
+    int32_t *__restrict__ far_all, double delta, int cross, const uint64_t *__restrict__ skeys,
+    const int64_t *__restrict__ sidx, const int64_t *__restrict__ rpos, int64_t E, double mrg,
+    int rev, unsigned long long *__restrict__ relax_total) {
     static_assert(S >= 1 && S <= 16, "1..16 sources per workgroup");
     // queue bits of the per-node mask; the near-far order needs S more bits for the
     // far pile (S <= 8 only: 16 sources fill the word)
@@ -506,7 +607,10 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     if (threadIdx.x == 0) s_relax = 0;
     unsigned long long relax = 0;
     const int64_t nbatch = (nsrc + S - 1) / S;
-    for (int64_t bi = blockIdx.x; bi < nbatch; bi += gridDim.x) {
+    for (int64_t bq = blockIdx.x; bq < nbatch; bq += gridDim.x) {
+        // rev: the batches from the last (the sources are in node order, i.e. by
+        // descending column count after the relabeling)
+        const int64_t bi = rev ? nbatch - 1 - bq : bq;
         if (threadIdx.x < S) {
             const int64_t si = bi * S + threadIdx.x;
             s_src[threadIdx.x] = si < nsrc ? sources[si] : -1;
@@ -859,17 +963,24 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                 __syncthreads();
             }
         }
-        // classify each source's unresolved targets
+        // classify each source's unresolved targets; with cross != 0 also the reverse
+        // columns (v, u) still open, from u's label of v (bb_cross_decide)
         for (int k = 0; k < S; ++k) {
             const int64_t u = s_src[k];
             if (u < 0) continue;
+            const double bk = s_wmax[k];  // >= 0: u's search ran dry within this bound
             for (int64_t j = optr[u] + threadIdx.x; j < optr[u + 1]; j += NT) {
                 const int64_t idx = order[j];
-                if (state[idx] != 0) continue;
+                const uint8_t st0 = state[idx];
+                if (st0 != 0 && !cross) continue;
+                const int64_t v = dst[idx];
                 const unsigned long long db = __hip_atomic_load(
-                    &dist[dst[idx] * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    &dist[v * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const double d = __longlong_as_double((long long)db);
-                state[idx] = ((db == kInfBits) || (w[idx] <= d + eps)) ? 1 : 2;
+                if (st0 == 0) state[idx] = ((db == kInfBits) || (w[idx] <= d + eps)) ? 1 : 2;
+                if (cross)
+                    bb_cross_decide<S>(skeys, sidx, rpos[idx], u, v, n, E, k, db, bk, mrg, eps, w, gp, gi,
+                                       gw, dist, state);
             }
         }
         __syncthreads();
@@ -1392,6 +1503,22 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                                                        touched, misc + 1);
                 } else {
                     uint32_t *fm = (uint32_t *)c->buf("bb_fmask").ensure(4 * slabs * n);
+                    // reverse-column decisions after every search (GSPARSE_BB_CROSS=0: off)
+                    int cross = 1;
+                    if (const char *e = getenv("GSPARSE_BB_CROSS")) cross = atoi(e) != 0;
+                    uint64_t *skeys = nullptr;
+                    int64_t *sidx = nullptr, *rpos = nullptr;
+                    if (cross) {
+                        skeys = (uint64_t *)c->buf("bb_skeys").ensure(8 * E);
+                        sidx = (int64_t *)c->buf("bb_sidx").ensure(8 * E);
+                        rpos = (int64_t *)c->buf("bb_rpos").ensure(8 * E);
+                        k_bb_pairkeys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, E, n, skeys, sidx);
+                        sort_pairs_u64_i64(c, skeys, sidx, E, bits_for_bb((uint64_t)n * (uint64_t)n));
+                        k_bb_revpos<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, E, n, skeys, rpos);
+                    }
+                    const double mrg = std::max(1e-8, 8.0 * (double)n * 0x1p-53);
+                    int rev = 0;  // GSPARSE_BB_ORDER=asc: lowest column counts first
+                    if (const char *e = getenv("GSPARSE_BB_ORDER")) rev = strcmp(e, "asc") == 0;
                     int32_t *farl = (int32_t *)c->buf("bb_far").ensure(8 * slabs * n);
                     auto *qm = (uint32_t *)qflag;
                     // near-far step: half the median edge weight (GSPARSE_BB_NEARFAR = the
@@ -1403,6 +1530,8 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
     k_bb_sssp_multi<NT_, S_><<<(unsigned)slabs, NT_, 0, s>>>(gp, gi, gw, n, sources, nsrc, optr, \
                                                             order, ddst, dw, eps, state, dist,  \
                                                             qm, fr, fm, touched, farl, delta, \
+                                                            cross, skeys, sidx, rpos, E, mrg, \
+                                                            rev, \
                                                             misc + 1)
                     if (bt == 1024) {
                         if (S == 2) GS_BBM(1024, 2); else if (S == 4) GS_BBM(1024, 4);
