@@ -384,7 +384,7 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
     Roman-like graph; costs = _scores_to_cost(Jaccard) as
     sparsify_metric_backbone passes them (core.py:251-279).  One step = the
     whole prune (graph build, witnesses, certificates, bounded searches) on
-    device-resident columns; N > 1 splits the source rows (u % N) and
+    device-resident columns; N > 1 splits the columns by pair (max(u, v) % N) and
     all-reduces the keep bytes."""
     import ctypes
 
@@ -459,7 +459,7 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
         "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (stand-in graph of the config's size; datasets are not downloadable here)",
         "config": {"workload": wl, "n": n, "E": E, "kept": kept,
-                   "parallelism": f"source-rows/{world}" if world > 1 else "1 GPU",
+                   "parallelism": f"column-pairs/{world}" if world > 1 else "1 GPU",
                    "graph_gen_s": round(t_gen, 2)},
         "roofline": roofline,
     }

@@ -9,8 +9,9 @@ SURVEY §8(e):
     score of both CSR entries of every pair (gs_jaccard_from_counts: the
     reference's single fp64 division) -- 2 B per directed edge on the wire
     instead of the 8 B per edge of a score all-gather.
-  * metric backbone: the per-source searches by source row (u % world), one
-    all-reduce(sum) of the uint8 keep bytes (each column has one contributor).
+  * metric backbone: the columns by pair (both directions of a pair on rank
+    max(u, v) % world), one all-reduce(sum) of the uint8 keep bytes (each
+    column has one contributor).
   * AA / degree / FeatCos (and Jaccard on explicit ranges): contiguous CSR
     edge ranges (equal counts, or equal per-edge work d_u + d_v for skewed
     graphs), then an all-gather of the fp64 scores so every rank can run the
@@ -232,9 +233,10 @@ def sharded_sparsify(engine, comm: Comm, scores, num_edges: int, retention_ratio
 
 def sharded_backbone(comm: Comm, edge_index: np.ndarray, num_nodes: int,
                      edge_weights: np.ndarray, epsilon: float = 1e-9, mask_fn=None) -> np.ndarray:
-    """metric_backbone keep mask with the per-source searches split over ranks
-    (source row u goes to rank u % world); one all-reduce(sum) of the keep
-    bytes -- each column is decided by exactly one rank."""
+    """metric_backbone keep mask with the columns split over ranks by pair (both
+    directions of pair {u, v} go to rank max(u, v) % world, ids as the library
+    labels them); one all-reduce(sum) of the keep bytes -- each column is decided
+    by exactly one rank."""
     from .metric_backbone import check_weights
 
     check_weights(edge_weights, np.asarray(edge_index).shape[1])

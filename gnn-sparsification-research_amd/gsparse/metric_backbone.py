@@ -47,8 +47,8 @@ def backbone_mask(edge_index: np.ndarray, num_nodes: int, edge_weights: np.ndarr
                   return_relax: bool = False, part: int = 0, nparts: int = 1):
     """Keep mask (bool[E]) of the metric backbone; device computation.
 
-    With nparts > 1 only the columns whose source row u has u % nparts == part
-    (u as the library labels it: graphs without id locality are relabeled by
+    With nparts > 1 only the columns (u, v) with max(u, v) % nparts == part (ids
+    as the library labels them: graphs without id locality are relabeled by
     degree first) are decided here (the rest read False): the parts OR to the
     whole mask."""
     ei = np.asarray(edge_index, dtype=np.int64)

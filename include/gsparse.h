@@ -209,8 +209,10 @@ int gs_metric_backbone(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src,
                        const int64_t *dst, const double *w, int64_t nw, int loc, double eps,
                        uint8_t *keep, int keep_loc, int64_t *n_relax);
 /* Part `part` of `nparts` of gs_metric_backbone (multi-GPU): keep
- * bytes of the columns whose source row u has u % nparts == part (their
- * searches run here), 0 elsewhere -- the element-wise sum over parts equals
+ * bytes of the columns (u, v) with max(u, v) % nparts == part -- both directions
+ * of a pair in one part, ids as the library labels them (graphs without id
+ * locality are relabeled by descending degree, so max(u, v) is the pair's
+ * lower-degree endpoint) -- 0 elsewhere; the element-wise sum over parts equals
  * the whole keep mask. */
 int gs_metric_backbone_part(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src,
                             const int64_t *dst, const double *w, int64_t nw, int loc, double eps,
