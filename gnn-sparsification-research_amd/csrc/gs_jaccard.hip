@@ -393,99 +393,40 @@ struct JacBitProbe {
 // a barrier).  The d_u of the owner and each entry's d_v give the union.
 // UL list elements per lane are loaded at once (the global reads are what the
 // loop waits on), then probed UP at a time (the probe state is what costs
-// registers); GS_JAC_SKIP: 64-element steps past the list's end are skipped as a
-// whole (wave-uniform) instead of run with every lane masked off.
-#ifndef GS_JAC_SKIP
-#define GS_JAC_SKIP 0
-#endif
-#ifndef GS_JAC_PIPE  // classes with the software-pipelined probe loop (bit k: class k)
-#define GS_JAC_PIPE 0x9  // class 0 and the two-per-CU 32K class
-#endif
-template <class Probe, int UL = kJacUnrollDef, int UP = UL, bool PIPE = false>
+// registers).  Measured and dropped (profiles/r04g_*, r04t_*): skipping the
+// all-masked 64-element steps, and a software-pipelined loop with the next
+// step's loads in flight during this step's probes (faster per class when run
+// alone, slower with the classes overlapping on their streams).
+template <class Probe, int UL = kJacUnrollDef, int UP = UL>
 __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix, int64_t du,
                                                  int64_t lo, const JacStage &st,
                                                  const JacSink &sk, const Probe &pr) {
     static_assert(UL % UP == 0, "probe groups split the loaded elements");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    // UL elements of one 64·UL-element step of an entry's list
-    auto load_step = [&](int64_t bb, int32_t dd, int32_t jj, int32_t(&out)[UL]) {
+    for (int k = wave; k < st.nbig; k += nw) {
+        const int64_t b = st.b[k];
+        const int32_t dv = __builtin_amdgcn_readfirstlane(st.dv[k]);
+        int64_t cnt = 0;
+        for (int32_t j0 = 0; j0 < dv; j0 += 64 * UL) {
+            int32_t xs[UL];  // all loads in flight before the first probe
 #pragma unroll
-        for (int t = 0; t < UL; ++t) {
-            const int32_t j = jj + t * 64 + lane;
-            out[t] = j < dd ? ix[bb + j] : -1;
-        }
-    };
-    auto probe_step = [&](const int32_t(&xs)[UL], int32_t j0, int32_t dv, int64_t &cnt) {
-#pragma unroll
-        for (int g = 0; g < UL; g += UP) {
-            if (GS_JAC_SKIP && j0 + g * 64 >= dv) break;
-            typename Probe::S ps[UP];
-#pragma unroll
-            for (int t = 0; t < UP; ++t) ps[t] = pr.first(xs[g + t] >= 0 ? xs[g + t] : 0);
-#pragma unroll
-            for (int t = 0; t < UP; ++t) {
-                const bool hit = xs[g + t] >= 0 && pr.done(xs[g + t], ps[t]);
-                cnt += __popcll(__ballot(hit));
+            for (int t = 0; t < UL; ++t) {
+                const int32_t j = j0 + t * 64 + lane;
+                xs[t] = j < dv ? ix[b + j] : -1;
             }
-        }
-    };
-    // PIPE: software-pipelined -- the list loads of the wave's next step (the rest of
-    // this entry, else its next entry) are in flight while this step's probes run
-    // (two list buffers of UL registers; where they fit the class's register budget:
-    // the 16K class would drop from three workgroups per CU to two)
-    if constexpr (PIPE) {
-        int k = wave;
-        int64_t b = 0, cnt = 0;
-        int32_t dv = 0, j0 = 0;
-        int32_t xs[UL];
-        if (k < st.nbig) {
-            b = st.b[k];
-            dv = __builtin_amdgcn_readfirstlane(st.dv[k]);
-            load_step(b, dv, 0, xs);
-        }
-        while (k < st.nbig) {
-            int kn = k;
-            int64_t bn = b;
-            int32_t dvn = dv, jn = j0 + 64 * UL;
-            if (jn >= dv) {
-                kn = k + nw;
-                jn = 0;
-                if (kn < st.nbig) {
-                    bn = st.b[kn];
-                    dvn = __builtin_amdgcn_readfirstlane(st.dv[kn]);
+#pragma unroll
+            for (int g = 0; g < UL; g += UP) {
+                typename Probe::S ps[UP];
+#pragma unroll
+                for (int t = 0; t < UP; ++t) ps[t] = pr.first(xs[g + t] >= 0 ? xs[g + t] : 0);
+#pragma unroll
+                for (int t = 0; t < UP; ++t) {
+                    const bool hit = xs[g + t] >= 0 && pr.done(xs[g + t], ps[t]);
+                    cnt += __popcll(__ballot(hit));
                 }
             }
-            int32_t xn[UL];
-            if (kn < st.nbig) {
-                load_step(bn, dvn, jn, xn);
-            } else {
-#pragma unroll
-                for (int t = 0; t < UL; ++t) xn[t] = -1;
-            }
-            probe_step(xs, j0, dv, cnt);
-            if (kn != k) {
-                if (lane == 0) sk.put(lo + st.off[k], cnt, du, dv);
-                cnt = 0;
-            }
-            k = kn;
-            b = bn;
-            dv = dvn;
-            j0 = jn;
-#pragma unroll
-            for (int t = 0; t < UL; ++t) xs[t] = xn[t];
         }
-    } else {
-        for (int k = wave; k < st.nbig; k += nw) {
-            const int64_t b = st.b[k];
-            const int32_t dv = __builtin_amdgcn_readfirstlane(st.dv[k]);
-            int64_t cnt = 0;
-            for (int32_t j0 = 0; j0 < dv; j0 += 64 * UL) {
-                int32_t xs[UL];  // all loads in flight before the first probe
-                load_step(b, dv, j0, xs);
-                probe_step(xs, j0, dv, cnt);
-            }
-            if (lane == 0) sk.put(lo + st.off[k], cnt, du, dv);
-        }
+        if (lane == 0) sk.put(lo + st.off[k], cnt, du, dv);
     }
     const int grp = lane >> 4, gl = lane & 15;
     const uint64_t gmask = 0xFFFFull << (16 * grp);
@@ -551,9 +492,7 @@ __global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ i
     }
     __syncthreads();
     constexpr int U = C >= 16384 ? GS_JAC_UNROLL_BIG : kJacUnrollDef;
-    constexpr int K = C == 2048 ? 0 : C == 8192 ? 1 : C == 16384 ? 2 : 3;  // row class
-    jac_probe_staged<JacHashProbe, U, U, ((GS_JAC_PIPE >> K) & 1) != 0>(ix, du, lo, st, sk,
-                                                                     JacHashProbe{tab, shift, mask});
+    jac_probe_staged<JacHashProbe, U>(ix, du, lo, st, sk, JacHashProbe{tab, shift, mask});
 }
 
 // Quotient tables (classes in GS_JAC_Q16, when the ids fit): 16-bit slots, so the
@@ -677,9 +616,8 @@ __global__ void __launch_bounds__(NT, MINW) k_jac_hashq(const int64_t *__restric
         jac_probe_staged<JacSortedProbe, 1>(ix, du, lo, st, sk, JacSortedProbe{ix + a, du});
     else
         jac_probe_staged<JacQProbe, (MINW >= 8 ? GS_JAC_LOADS_Q8 : GS_JAC_UNROLL_BIG),
-                         (MINW >= 8 ? GS_JAC_UNROLL_Q8 : GS_JAC_UNROLL_BIG),
-                         (((GS_JAC_PIPE >> (MINW >= 8 ? 3 : 1)) & 1) != 0)>(ix, du, lo, st, sk,
-                                                                            JacQProbe{tab, qp, NB - 1});
+                         (MINW >= 8 ? GS_JAC_UNROLL_Q8 : GS_JAC_UNROLL_BIG)>(ix, du, lo, st, sk,
+                                                                             JacQProbe{tab, qp, NB - 1});
 }
 
 // quotient-table parameters for C 16-bit slots and ids < n; false when the

@@ -146,7 +146,8 @@ int gs_feature_cosine_f64(gs_ctx *ctx, const double *x, int64_t f, int x_loc, in
  * gs_er_project_pcg64: the same, drawing the normals on the device from
  *   NumPy's PCG64 state (state_hi/lo, inc_hi/lo) with NumPy's ziggurat.
  * gs_er_solve: CG on columns [col0, col1) (:284-289), SciPy 1.15 cg
- *   recurrence with OpenBLAS-SkylakeX ddot order for blas_threads threads.
+ *   recurrence with OpenBLAS-SkylakeX ddot order for blas_threads threads
+ *   (more than 64 run as 64: OpenBLAS's MAX_THREADS in NumPy's build).
  * gs_er_scores: out[e-e0] = sum over columns [col0,col1) of (Z_u - Z_v)^2 in
  *   NumPy pairwise order (:292-293).  [col0,col1) must be a node of the
  *   pairwise tree of k (the whole range, or a gs_er_split() block); when
