@@ -393,10 +393,13 @@ struct JacBitProbe {
 // a barrier).  The d_u of the owner and each entry's d_v give the union.
 // UL list elements per lane are loaded at once (the global reads are what the
 // loop waits on), then probed UP at a time (the probe state is what costs
-// registers).  Measured and dropped (profiles/r04g_*, r04t_*): skipping the
-// all-masked 64-element steps, and a software-pipelined loop with the next
-// step's loads in flight during this step's probes (faster per class when run
-// alone, slower with the classes overlapping on their streams).
+// registers).  Measured and dropped (profiles/r04g_*, r04t_*, r04u_*): skipping
+// the all-masked 64-element steps; a software-pipelined loop with the next step's
+// loads in flight during this step's probes; and cutting long lists into chunks
+// the waves take in turn (the slowest wave of a 16K / 32K task had ~1.45x the mean
+// steps) -- the last two are 6-14 % faster per class run alone and 2-6 % slower
+// with the classes overlapping on their streams, which fill each other's idle
+// waves already.
 template <class Probe, int UL = kJacUnrollDef, int UP = UL>
 __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix, int64_t du,
                                                  int64_t lo, const JacStage &st,
