@@ -927,3 +927,37 @@ def test_backbone_near_far_order(gs, nearfar, monkeypatch):
         single = backbone_mask(ei, n, w)
         monkeypatch.setenv("GSPARSE_BB_MULTI", "8")
         assert np.array_equal(multi, single)
+
+
+@pytest.mark.parametrize("weights", ["ties", "scales", "asymmetric"])
+@pytest.mark.parametrize("order", ["asc", "desc"])
+def test_backbone_reverse_columns_vs_oracle(gs, weights, order, monkeypatch):
+    """The reverse-column decisions of k_bb_sssp_multi (gs_backbone.hip
+    bb_cross_decide) on weights that stress their margins: small integers (exact
+    ties between an edge and a 2- or 3-edge path, where neither the prune nor the
+    exact certificate may fire), costs over 18 decades (fl folds of very different
+    magnitudes), and different weights on the two directions of a pair -- 16 sources
+    per workgroup in either batch order, against the oracle's per-row Dijkstra
+    (metric_backbone.py:86-111), with epsilon 0 and the default."""
+    from gsparse import graphs
+    from gsparse.metric_backbone import backbone_mask
+
+    monkeypatch.setenv("GSPARSE_BB_MULTI", "16")
+    monkeypatch.setenv("GSPARSE_BB_ORDER", order)
+    rng = np.random.default_rng(7)
+    ei, n = graphs.rmat(12, 8, seed=5), 1 << 12
+    E = ei.shape[1]
+    # one weight per undirected pair, then the asymmetric case perturbs one direction
+    key = np.minimum(ei[0], ei[1]) * n + np.maximum(ei[0], ei[1])
+    _, inv = np.unique(key, return_inverse=True)
+    if weights == "ties":
+        pw = rng.integers(1, 4, size=inv.max() + 1).astype(np.float64)
+    else:
+        pw = 10.0 ** rng.uniform(-9, 9, size=inv.max() + 1)
+    w = pw[inv]
+    if weights == "asymmetric":
+        flip = rng.random(E) < 0.3
+        w = np.where(flip, w * rng.uniform(0.5, 2.0, size=E), w)
+    for eps in (1e-9, 0.0):
+        ref = O.metric_backbone(ei, n, w, epsilon=eps)
+        assert np.array_equal(backbone_mask(ei, n, w, epsilon=eps), ref), (weights, order, eps)
