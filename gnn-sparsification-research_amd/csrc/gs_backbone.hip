@@ -583,7 +583,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     int32_t *__restrict__ fr_all, uint32_t *__restrict__ fm_all, int32_t *__restrict__ touched_all,
     int32_t *__restrict__ far_all, double delta, int cross, const uint64_t *__restrict__ skeys,
     const int64_t *__restrict__ sidx, const int64_t *__restrict__ rpos, int64_t E, double mrg,
-    int rev, unsigned long long *__restrict__ relax_total) {
+    int rev, unsigned long long *__restrict__ batch_next,
+    unsigned long long *__restrict__ relax_total) {
     static_assert(S >= 1 && S <= 16, "1..16 sources per workgroup");
     // queue bits of the per-node mask; the near-far order needs S more bits for the
     // far pile (S <= 8 only: 16 sources fill the word)
@@ -615,7 +616,13 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     if (threadIdx.x == 0) s_relax = 0;
     unsigned long long relax = 0;
     const int64_t nbatch = (nsrc + S - 1) / S;
-    for (int64_t bq = blockIdx.x; bq < nbatch; bq += gridDim.x) {
+    // batches taken in order from a global counter as workgroups free up (batch_next;
+    // null: static striding), so the long searches at the end of the order do not
+    // leave workgroups idle behind a fixed share
+    __shared__ long long s_bq;
+    if (threadIdx.x == 0) s_bq = batch_next ? (long long)atomicAdd(batch_next, 1ull) : (long long)blockIdx.x;
+    __syncthreads();
+    for (int64_t bq = s_bq; bq < nbatch; bq = s_bq) {
         // rev: the batches from the last (the sources are in node order, i.e. by
         // descending column count after the relabeling)
         const int64_t bi = rev ? nbatch - 1 - bq : bq;
@@ -999,6 +1006,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
             for (int k = 0; k < S; ++k) dist[(int64_t)y * S + k] = kInfBits;
             qmask[y] = 0u;
         }
+        if (threadIdx.x == 0)
+            s_bq = batch_next ? (long long)atomicAdd(batch_next, 1ull) : (long long)(bq + gridDim.x);
         __syncthreads();
     }
     atomicAdd(&s_relax, relax);
@@ -1527,6 +1536,10 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                     // GSPARSE_BB_ORDER=desc: hubs first)
                     int rev = 1;
                     if (const char *e = getenv("GSPARSE_BB_ORDER")) rev = strcmp(e, "desc") != 0;
+                    // batches from a global counter (misc + 2, zeroed with misc);
+                    // GSPARSE_BB_DYNAMIC=0: static striding
+                    unsigned long long *bnext = misc + 2;
+                    if (const char *e = getenv("GSPARSE_BB_DYNAMIC")) bnext = atoi(e) != 0 ? bnext : nullptr;
                     int32_t *farl = (int32_t *)c->buf("bb_far").ensure(8 * slabs * n);
                     auto *qm = (uint32_t *)qflag;
                     // near-far step: half the median edge weight (GSPARSE_BB_NEARFAR = the
@@ -1539,7 +1552,7 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                                                             order, ddst, dw, eps, state, dist,  \
                                                             qm, fr, fm, touched, farl, delta, \
                                                             cross, skeys, sidx, rpos, E, mrg, \
-                                                            rev, \
+                                                            rev, bnext, \
                                                             misc + 1)
                     if (bt == 1024) {
                         if (S == 2) GS_BBM(1024, 2); else if (S == 4) GS_BBM(1024, 4);
