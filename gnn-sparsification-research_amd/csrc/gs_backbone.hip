@@ -447,8 +447,9 @@ __device__ __forceinline__ bool bb_min_improves(unsigned long long *p, unsigned 
 //    but the edge itself from below: real length >= A (1 - m).  A (1 - 3m) > D then
 //    means the edge is the only shortest path from either end by more than any
 //    rounding, so d_fl(v, u) = fl(0 + w_G) = D exactly, and the reverse column is
-//    decided as the reference decides it: w <= D + eps.  (v of more than kBbCrossDeg
-//    neighbours is left to its own search.)
+//    decided as the reference decides it: w <= D + eps.  (A v of more than
+//    kBbCrossDeg neighbours -- a hub the search reached -- is scanned by the whole
+//    workgroup after the classification, up to kBbCrossBig of them per batch.)
 //  * keep, v unreached: d_fl(u, v) > bk, so w <= (bk (1 - m) + eps)(1 - m) keeps it.
 // Whatever falls within the margins stays open for v's own search.
 // skeys / sidx: every column's (row * n + col) key in ascending order and its column;
@@ -457,8 +458,9 @@ __device__ __forceinline__ bool bb_min_improves(unsigned long long *p, unsigned 
 #define GS_BB_CROSS_DEG 512
 #endif
 static constexpr int64_t kBbCrossDeg = GS_BB_CROSS_DEG;
+static constexpr int kBbCrossBig = 256;
 template <int S>
-__device__ __forceinline__ void bb_cross_decide(const uint64_t *__restrict__ skeys,
+__device__ __forceinline__ bool bb_cross_decide(const uint64_t *__restrict__ skeys,
                                                 const int64_t *__restrict__ sidx, int64_t rp,
                                                 int64_t u, int64_t v, int64_t n, int64_t E,
                                                 int k, unsigned long long db, double bk, double m,
@@ -468,15 +470,16 @@ __device__ __forceinline__ void bb_cross_decide(const uint64_t *__restrict__ ske
                                                 const double *__restrict__ gw,
                                                 const unsigned long long *__restrict__ dist,
                                                 uint8_t *__restrict__ state) {
-    if (rp < 0) return;
+    if (rp < 0) return false;
     const uint64_t rkey = (uint64_t)v * (uint64_t)n + (uint64_t)u;
     bool open = false;  // any reverse column still undecided
     for (int64_t p = rp; p < E && skeys[p] == rkey; ++p) open = open || state[sidx[p]] == 0;
-    if (!open) return;
+    if (!open) return false;
     const bool reached = db != kInfBits;
     const double D = __longlong_as_double((long long)db);
     bool exact = false;
-    if (reached && bk >= 0.0 && D <= bk && gp[v + 1] - gp[v] <= kBbCrossDeg) {
+    const bool eligible = reached && bk >= 0.0 && D <= bk;
+    if (eligible && gp[v + 1] - gp[v] <= kBbCrossDeg) {
         double A = __longlong_as_double((long long)kInfBits);
         for (int64_t e = gp[v]; e < gp[v + 1]; ++e) {
             const int32_t x = gi[e];
@@ -493,6 +496,7 @@ __device__ __forceinline__ void bb_cross_decide(const uint64_t *__restrict__ ske
     const double hi = reached ? (D * (1.0 + m) + eps) * (1.0 + m) : 0.0;
     const bool keep_unreached = !reached && bk >= 0.0;
     const double lo = keep_unreached ? (bk * (1.0 - m) + eps) * (1.0 - m) : -1.0;
+    bool left = false;
     for (int64_t p = rp; p < E && skeys[p] == rkey; ++p) {
         const int64_t r = sidx[p];
         if (state[r] != 0) continue;
@@ -500,7 +504,10 @@ __device__ __forceinline__ void bb_cross_decide(const uint64_t *__restrict__ ske
         if (exact) state[r] = wr <= D + eps ? 1 : 2;
         else if (reached && wr > hi) state[r] = 2;
         else if (keep_unreached && wr <= lo) state[r] = 1;
+        else left = true;
     }
+    // a v of more than kBbCrossDeg neighbours: the caller's workgroup scans them
+    return left && eligible && gp[v + 1] - gp[v] > kBbCrossDeg;
 }
 
 // (row * n + col) key of every column, for the reverse-column lookup
@@ -592,7 +599,9 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     constexpr bool NF = S <= 8;
     if (!NF) delta = 0.0;
     constexpr int NW = NT / 64;
-    __shared__ int s_fcount, s_ncount, s_tcount, s_nfar, s_nfar2, s_farleft, s_nheavy;
+    __shared__ int s_fcount, s_ncount, s_tcount, s_nfar, s_nfar2, s_farleft, s_nheavy, s_nbig;
+    __shared__ int64_t s_big[kBbCrossBig];  // deferred reverse decisions: idx << 4 | source k
+    __shared__ unsigned long long s_amin;
     __shared__ int32_t s_heavy[kBbHeavyMax];
     __shared__ uint32_t s_hmask[kBbHeavyMax];
     __shared__ uint32_t s_nearany;
@@ -673,6 +682,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
             s_nfar = 0;
             s_farleft = 0;
             s_nearany = 0;
+            s_nbig = 0;
+            s_amin = kInfBits;
         }
         __syncthreads();
         int32_t *cur = fa, *nxt = fb;
@@ -993,9 +1004,55 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                     &dist[v * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const double d = __longlong_as_double((long long)db);
                 if (st0 == 0) state[idx] = ((db == kInfBits) || (w[idx] <= d + eps)) ? 1 : 2;
-                if (cross)
+                if (cross &&
                     bb_cross_decide<S>(skeys, sidx, rpos[idx], u, v, n, E, k, db, bk, mrg, eps, w, gp, gi,
-                                       gw, dist, state);
+                                       gw, dist, state)) {
+                    const int q = atomicAdd(&s_nbig, 1);
+                    if (q < kBbCrossBig) s_big[q] = (idx << 4) | k;
+                }
+            }
+        }
+        __syncthreads();
+        // deferred exact reverse decisions (targets of many neighbours): the workgroup
+        // takes the lower bound A over v's neighbours together (bb_cross_decide's rule)
+        {
+            const int nbg = s_nbig < kBbCrossBig ? s_nbig : kBbCrossBig;
+            for (int q = 0; q < nbg; ++q) {
+                const int64_t idx = s_big[q] >> 4;
+                const int k = (int)(s_big[q] & 15);
+                const int64_t u = s_src[k], v = dst[idx];
+                const double bk = s_wmax[k];
+                double a = __longlong_as_double((long long)kInfBits);
+                for (int64_t e = gp[v] + threadIdx.x; e < gp[v + 1]; e += NT) {
+                    const int32_t x = gi[e];
+                    if (x == u) continue;
+                    const unsigned long long bx = __hip_atomic_load(&dist[(int64_t)x * S + k], __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const double dx = __longlong_as_double((long long)bx);
+                    const double lb = ((bx != kInfBits && dx <= bk) ? dx : bk) + gw[e];
+                    a = lb < a ? lb : a;
+                }
+                for (int off = 32; off > 0; off >>= 1) {
+                    const double o = __shfl_xor(a, off, 64);
+                    a = o < a ? o : a;
+                }
+                if ((threadIdx.x & 63) == 0)  // a >= 0: its bits order as the values
+                    atomicMin(&s_amin, (unsigned long long)__double_as_longlong(a));
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    const double A = __longlong_as_double((long long)s_amin);
+                    const double D = __longlong_as_double((long long)__hip_atomic_load(
+                        &dist[v * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                    if (A * (1.0 - 3.0 * mrg) > D) {
+                        const uint64_t rkey = (uint64_t)v * (uint64_t)n + (uint64_t)u;
+                        for (int64_t p = rpos[idx]; p < E && skeys[p] == rkey; ++p) {
+                            const int64_t r = sidx[p];
+                            if (state[r] == 0) state[r] = w[r] <= D + eps ? 1 : 2;
+                        }
+                    }
+                    s_amin = kInfBits;
+                }
+                __syncthreads();
             }
         }
         __syncthreads();
