@@ -455,10 +455,13 @@ __device__ __forceinline__ bool bb_min_improves(unsigned long long *p, unsigned 
 // skeys / sidx: every column's (row * n + col) key in ascending order and its column;
 // rp: the first position of the reverse key (-1: none).
 #ifndef GS_BB_CROSS_DEG
-#define GS_BB_CROSS_DEG 512
+#define GS_BB_CROSS_DEG 128
 #endif
 static constexpr int64_t kBbCrossDeg = GS_BB_CROSS_DEG;
-static constexpr int kBbCrossBig = 256;
+#ifndef GS_BB_CROSS_BIG
+#define GS_BB_CROSS_BIG 1024
+#endif
+static constexpr int kBbCrossBig = GS_BB_CROSS_BIG;
 template <int S>
 __device__ __forceinline__ bool bb_cross_decide(const uint64_t *__restrict__ skeys,
                                                 const int64_t *__restrict__ sidx, int64_t rp,
