@@ -1474,7 +1474,9 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
             prof_end(c, tp, "bb_witness", 0.0);
             tp = prof_begin(c);
             // landmark / degree-1 certificates (GSPARSE_BB_LANDMARKS = K, 0 = off)
-            int K = 16;
+            // (large graphs: 48 -- with the reverse-column decisions the searches are
+            // what the certificates leave, RMAT-18 711 vs 725 ms at 16; 0: 2.17 s)
+            int K = n > 65536 ? 48 : 16;
             if (const char *e = getenv("GSPARSE_BB_LANDMARKS")) K = atoi(e) < 0 ? 0 : atoi(e);
             if (K > n) K = (int)n;
             // landmark ids: host source of an async copy, alive until the stream sync below
@@ -1538,16 +1540,19 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
             if (nsrc > 0) {
                 int64_t *sources = (int64_t *)b_sources.ensure(8 * nsrc);
                 k_bb_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(flag, pos, n, sources);
-                // large graphs (big search balls): one 1024-thread workgroup per CU (RMAT-18:
-                // 4.1 s; 1,024 x 256 threads 5.2 s, 512 x 512 4.4 s, 128 x 1,024 5.9 s); small
-                // ones (many short searches): 1,024 workgroups of 256 (Roman: 2.2 vs 3.0 ms)
+                // large graphs (big search balls): 512 workgroups of 512 threads, two per CU
+                // (RMAT-18 with the final search: 650 vs 692 ms for 256 x 1,024; round 1's
+                // plain search preferred 256 x 1,024); small ones (many short searches):
+                // 1,024 workgroups of 256 (Roman: 2.2 vs 3.0 ms)
                 const bool big = n > 65536;
-                int64_t maxslabs = big ? 256 : 1024;
+                int64_t maxslabs = big ? 512 : 1024;
                 if (const char *e = getenv("GSPARSE_BB_SLABS")) maxslabs = atoi(e) > 0 ? atoi(e) : maxslabs;
                 // sources searched together per workgroup (k_bb_sssp_multi), 1 = alone: 8 on
-                // large graphs (RMAT-18: 2.81 s vs 3.07 s alone; 4 sources 3.14 s), alone on
-                // small ones (Roman: 2.30 ms vs 2.45 ms with 8)
-                int S = big ? 16 : 1;
+                // large graphs, with the near-far order (RMAT-18: 692 ms; 16 sources, which
+                // leave no mask bits for the far pile, 725 ms -- before the reverse-column
+                // decisions 16 led, 1.85 vs 2.15 s), alone on small ones (Roman: 2.30 ms vs
+                // 2.45 ms with 8)
+                int S = big ? 8 : 1;
                 if (const char *e = getenv("GSPARSE_BB_MULTI")) {
                     const int v = atoi(e);
                     S = v >= 16 ? 16 : v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
@@ -1567,7 +1572,7 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                 k_bb_fill_u64<<<grid_for((int64_t)S * slabs * n, 256, 65536), 256, 0, s>>>(
                     dist, (int64_t)S * slabs * n, kInfBits);
                 GS_HIP(hipMemsetAsync(qflag, 0, 4 * slabs * n, s));
-                int bt = big ? 1024 : 256;
+                int bt = big ? 512 : 256;
                 if (const char *e = getenv("GSPARSE_BB_THREADS")) bt = atoi(e) == 1024 ? 1024 : atoi(e) == 512 ? 512 : 256;
                 if (S == 1) {
                     auto kfn = bt == 1024 ? k_bb_sssp<1024> : bt == 512 ? k_bb_sssp<512> : k_bb_sssp<256>;
@@ -1602,9 +1607,10 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
                     if (const char *e = getenv("GSPARSE_BB_DYNAMIC")) bnext = atoi(e) != 0 ? bnext : nullptr;
                     int32_t *farl = (int32_t *)c->buf("bb_far").ensure(8 * slabs * n);
                     auto *qm = (uint32_t *)qflag;
-                    // near-far step: half the median edge weight (GSPARSE_BB_NEARFAR = the
-                    // factor, 0 = plain frontier order)
-                    double nfs = 0.5;
+                    // near-far step: twice the median edge weight (GSPARSE_BB_NEARFAR = the
+                    // factor, 0 = plain frontier order; RMAT-18: 1 / 2 / 4 -> 687 / 692 / 700 ms
+                    // at 256 x 1,024 threads, 0 -> 723 ms)
+                    double nfs = 2.0;
                     if (const char *e = getenv("GSPARSE_BB_NEARFAR")) nfs = atof(e);
                     const double delta = nfs > 0.0 && wmed > 0.0 ? nfs * wmed : 0.0;
 #define GS_BBM(NT_, S_)                                                                        \

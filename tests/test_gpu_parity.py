@@ -931,18 +931,19 @@ def test_backbone_near_far_order(gs, nearfar, monkeypatch):
 
 @pytest.mark.parametrize("weights", ["ties", "scales", "asymmetric"])
 @pytest.mark.parametrize("order", ["asc", "desc"])
-def test_backbone_reverse_columns_vs_oracle(gs, weights, order, monkeypatch):
+@pytest.mark.parametrize("S", ["8", "16"])
+def test_backbone_reverse_columns_vs_oracle(gs, weights, order, S, monkeypatch):
     """The reverse-column decisions of k_bb_sssp_multi (gs_backbone.hip
     bb_cross_decide) on weights that stress their margins: small integers (exact
     ties between an edge and a 2- or 3-edge path, where neither the prune nor the
     exact certificate may fire), costs over 18 decades (fl folds of very different
-    magnitudes), and different weights on the two directions of a pair -- 16 sources
-    per workgroup in either batch order, against the oracle's per-row Dijkstra
+    magnitudes), and different weights on the two directions of a pair -- 8 (near-far)
+    or 16 sources per workgroup in either batch order, against the oracle's per-row Dijkstra
     (metric_backbone.py:86-111), with epsilon 0 and the default."""
     from gsparse import graphs
     from gsparse.metric_backbone import backbone_mask
 
-    monkeypatch.setenv("GSPARSE_BB_MULTI", "16")
+    monkeypatch.setenv("GSPARSE_BB_MULTI", S)  # 8: with the near-far order (default step)
     monkeypatch.setenv("GSPARSE_BB_ORDER", order)
     rng = np.random.default_rng(7)
     ei, n = graphs.rmat(12, 8, seed=5), 1 << 12

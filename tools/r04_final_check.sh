@@ -13,3 +13,5 @@ tail -1 "$OUT/smoke.log"
 timeout -k 10 300 python bench.py > "$OUT/bench_roman.json" 2> "$OUT/bench_roman.err" || exit $?
 python3 -c "import json;a=json.load(open('$OUT/bench_roman.json'));print('roman ms/step',a['ms_per_step'])"
 tools/r04z_profiles.sh "$OUT/prof" roman rmat backbone arxiv || exit $?
+timeout -k 10 600 python tools/bb_probe.py 18 1 > "$OUT/bb_probe.json" 2> "$OUT/bb_probe.err" || exit $?
+tail -1 "$OUT/bb_probe.json" | cut -c1-1500

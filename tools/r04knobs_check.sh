@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-4 knobs: the backbone's landmark count and sources per workgroup (with the
+# near-far order at 8) on the final code, RMAT-18 whole prune.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=${1:-gpurun_out/r04knobs}
+mkdir -p "$OUT"
+run() {
+  env "$@" timeout -k 10 200 python tools/bb_probe.py 18 1 whole > "$OUT/bb.json" 2> "$OUT/bb.err" || exit $?
+  echo "$*: $(head -1 $OUT/bb.json)"
+}
+run GSPARSE_BB_MULTI=8 GSPARSE_BB_NEARFAR=2 GSPARSE_BB_THREADS=512 GSPARSE_BB_SLABS=512
+run GSPARSE_BB_MULTI=8 GSPARSE_BB_NEARFAR=2 GSPARSE_BB_LANDMARKS=48
+run GSPARSE_BB_MULTI=8 GSPARSE_BB_NEARFAR=2 GSPARSE_BB_THREADS=512 GSPARSE_BB_SLABS=512 GSPARSE_BB_LANDMARKS=48
+run GSPARSE_BB_MULTI=8 GSPARSE_BB_NEARFAR=1
+run GSPARSE_BB_MULTI=8 GSPARSE_BB_NEARFAR=4
+run GSPARSE_BB_THREADS=512 GSPARSE_BB_SLABS=512 GSPARSE_BB_LANDMARKS=48
+run GSPARSE_BB_MULTI=8 GSPARSE_BB_NEARFAR=2 GSPARSE_BB_THREADS=512 GSPARSE_BB_SLABS=768
