@@ -9,10 +9,11 @@ run() {
   env "$@" timeout -k 10 200 python tools/bb_probe.py 18 1 whole > "$OUT/bb.json" 2> "$OUT/bb.err" || exit $?
   echo "$*: $(head -1 $OUT/bb.json)"
 }
-run GSPARSE_BB_MULTI=8 GSPARSE_BB_NEARFAR=2 GSPARSE_BB_THREADS=512 GSPARSE_BB_SLABS=512
-run GSPARSE_BB_MULTI=8 GSPARSE_BB_NEARFAR=2 GSPARSE_BB_LANDMARKS=48
-run GSPARSE_BB_MULTI=8 GSPARSE_BB_NEARFAR=2 GSPARSE_BB_THREADS=512 GSPARSE_BB_SLABS=512 GSPARSE_BB_LANDMARKS=48
-run GSPARSE_BB_MULTI=8 GSPARSE_BB_NEARFAR=1
-run GSPARSE_BB_MULTI=8 GSPARSE_BB_NEARFAR=4
-run GSPARSE_BB_THREADS=512 GSPARSE_BB_SLABS=512 GSPARSE_BB_LANDMARKS=48
-run GSPARSE_BB_MULTI=8 GSPARSE_BB_NEARFAR=2 GSPARSE_BB_THREADS=512 GSPARSE_BB_SLABS=768
+run GSPARSE_BB_LANDMARKS=48
+run GSPARSE_BB_NEARFAR=1
+run GSPARSE_BB_NEARFAR=3
+run GSPARSE_BB_LANDMARKS=96
+run GSPARSE_BB_LANDMARKS=32
+run GSPARSE_BB_SLABS=768
+run GSPARSE_BB_THREADS=256 GSPARSE_BB_SLABS=1024
+run GSPARSE_BB_MULTI=4
