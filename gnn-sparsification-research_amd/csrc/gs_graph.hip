@@ -261,7 +261,7 @@ int gs_graph_from_edge_index(gs_ctx *c, int64_t n, int64_t E, const int64_t *src
                                   c->stream));
             GS_HIP(hipStreamSynchronize(c->stream));
             nnz = last[0] + last[1];
-            g.indices.ensure(sizeof(int32_t) * nnz);
+            g.indices.ensure(sizeof(int32_t) * (nnz + kIxPad));
             g.rows.ensure(sizeof(int32_t) * nnz);
             g.data.ensure(sizeof(double) * nnz);
             int64_t *start = (int64_t *)c->scratch[3].ensure(sizeof(int64_t) * nnz);
@@ -287,7 +287,7 @@ int gs_graph_from_csr(gs_ctx *c, int64_t n, int64_t nnz, const int64_t *indptr,
         g.n = n;
         g.nnz = nnz;
         int64_t *ip = (int64_t *)g.indptr.ensure(sizeof(int64_t) * (n + 1));
-        g.indices.ensure(sizeof(int32_t) * (nnz ? nnz : 1));
+        g.indices.ensure(sizeof(int32_t) * (nnz + kIxPad));
         g.data.ensure(sizeof(double) * (nnz ? nnz : 1));
         g.rows.ensure(sizeof(int32_t) * (nnz ? nnz : 1));
         GS_HIP(hipMemcpyAsync(ip, indptr, sizeof(int64_t) * (n + 1),

@@ -80,6 +80,9 @@ struct ProfPending {
     double its_bytes = 0.0;
 };
 static constexpr int kProfPendingMax = 4096;
+// int32 entries allocated past the last column index: the Jaccard probe loop reads
+// lists in unconditional 64-lane steps (up to 511 entries past a list's end, masked)
+static constexpr int64_t kIxPad = 1024;
 
 struct Graph {
     int64_t n = 0, nnz = 0;

@@ -405,18 +405,26 @@ __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
                                                  int64_t lo, const JacStage &st,
                                                  const JacSink &sk, const Probe &pr) {
     static_assert(UL % UP == 0, "probe groups split the loaded elements");
+    static_assert(64 * UL <= kIxPad, "unconditional list steps stay inside the index padding");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     for (int k = wave; k < st.nbig; k += nw) {
-        const int64_t b = st.b[k];
         const int32_t dv = __builtin_amdgcn_readfirstlane(st.dv[k]);
+        // the list's base is wave-uniform: loads from a scalar base, one lane offset and
+        // immediate step offsets, unconditional -- the ones past d_v read the next rows'
+        // entries (or the kIxPad padding after the last row) and are masked
+        const uint64_t lb = (uint64_t)(ix + st.b[k]);
+        using gi32 = __attribute__((address_space(1))) const int32_t;  // global, not flat
+        gi32 *lst = (gi32 *)(
+            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lb) |
+            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lb >> 32)) << 32);
         int64_t cnt = 0;
         for (int32_t j0 = 0; j0 < dv; j0 += 64 * UL) {
             int32_t xs[UL];  // all loads in flight before the first probe
+            gi32 *lp = lst + (uint32_t)(j0 + lane);
 #pragma unroll
-            for (int t = 0; t < UL; ++t) {
-                const int32_t j = j0 + t * 64 + lane;
-                xs[t] = j < dv ? ix[b + j] : -1;
-            }
+            for (int t = 0; t < UL; ++t) xs[t] = lp[t * 64];
+#pragma unroll
+            for (int t = 0; t < UL; ++t) xs[t] = lane + t * 64 < dv - j0 ? xs[t] : -1;
 #pragma unroll
             for (int g = 0; g < UL; g += UP) {
                 typename Probe::S ps[UP];
