@@ -1449,8 +1449,9 @@ extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const in
         unsigned long long *misc = (unsigned long long *)b_misc.ensure(64);
         GS_HIP(hipMemsetAsync(misc, 0, 64, s));
         int64_t relax = 0;
-        hipEvent_t t0 = prof_begin(c), tall = prof_begin(c);
+        hipEvent_t tall = prof_begin(c);
         if (E > 0) {
+            hipEvent_t t0 = prof_begin(c);  // ended as "bb_build" below (no leak at E = 0)
             int64_t *gp;
             int32_t *gi;
             double *gw;

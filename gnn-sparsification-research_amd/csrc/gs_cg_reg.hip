@@ -433,6 +433,9 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
         GS_HIP(hipHostMalloc((void **)&c->split_abort_host, sizeof(int32_t), hipHostMallocDefault));
         GS_HIP(hipEventCreateWithFlags(&c->split_abort_ev, hipEventDisableTiming));
     }
+    // the previous split launch's word must be read before its pinned slot is reused
+    // (ADVICE r04): the copy may still be pending when a new launch is queued
+    if (c->split_abort_pending) split_abort_poll(c, true);
     *c->split_abort_host = 0;
     GS_HIP(hipMemcpyAsync(c->split_abort_host, B.abortf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     GS_HIP(hipEventRecord(c->split_abort_ev, s));

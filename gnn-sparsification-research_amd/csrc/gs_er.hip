@@ -1642,6 +1642,15 @@ void project_rows(gs_ctx *c, int64_t e0, int64_t e1, const double *draw, int64_t
 
 using namespace gs;
 
+// every column of [c0, c1) solved since the last gs_er_prepare (a read of
+// columns another rank -- or no one -- solved must not return stale X)
+static bool er_cols_solved(const ErState &er, int64_t c0, int64_t c1) {
+    if ((int64_t)er.col_solved.size() < c1) return false;
+    for (int64_t i = c0; i < c1; ++i)
+        if (!er.col_solved[i]) return false;
+    return true;
+}
+
 extern "C" {
 
 int gs_er_prepare(gs_ctx *c, int64_t k, double reg, int64_t *m_out) {
@@ -1662,7 +1671,12 @@ int gs_er_prepare(gs_ctx *c, int64_t k, double reg, int64_t *m_out) {
         int64_t regbits;
         memcpy(&regbits, &reg, sizeof(regbits));
         const std::vector<int64_t> pkey = {g.epoch, k, regbits};
+        er.col_solved.assign((size_t)k, 0);
         if (pkey == er.prep_key) {
+            // per-column scalars and iteration counts restart (async, no host sync): a
+            // column not solved since this prepare reports 0 iterations, as before
+            GS_HIP(hipMemsetAsync(er.colstate.ptr, 0, er.colstate.bytes, c->stream));
+            GS_HIP(hipMemsetAsync(er.iters.ptr, 0, sizeof(int32_t) * k, c->stream));
             if (m_out) *m_out = er.m;
             return;
         }
@@ -1734,9 +1748,10 @@ int gs_er_prepare(gs_ctx *c, int64_t k, double reg, int64_t *m_out) {
         er.Q.ensure(nk);
         // the projection writes every Y entry it covers (the first rows fold from 0.0);
         // the row padding past k is zeroed once per allocation
-        if (er.rr_zeroed != er.Rr.ptr || er.Rr.bytes < nk) {
+        if (er.rr_zeroed != er.Rr.ptr || er.rr_k != k) {
             GS_HIP(hipMemsetAsync(er.Rr.ptr, 0, er.Rr.bytes, c->stream));
             er.rr_zeroed = er.Rr.ptr;
+            er.rr_k = k;
         }
         er.colstate.ensure(sizeof(double) * 5 * k + sizeof(int32_t) * (3 * k + 4));
         GS_HIP(hipMemsetAsync(er.colstate.ptr, 0, er.colstate.bytes, c->stream));
@@ -2070,6 +2085,7 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
             }
             er.pcur = 0;
             er.solved = true;
+            std::fill(er.col_solved.begin() + col0, er.col_solved.begin() + col1, 1);
             return;
         }
         GS_HIP(hipMemsetAsync(cp.nactive, 0, sizeof(int32_t), c->stream));
@@ -2193,6 +2209,7 @@ int gs_er_solve(gs_ctx *c, int64_t col0, int64_t col1, int32_t maxiter, double r
                               c->stream));
         GS_HIP(hipStreamSynchronize(c->stream));
         er.solved = true;
+        std::fill(er.col_solved.begin() + col0, er.col_solved.begin() + col1, 1);
     });
 }
 
@@ -2204,6 +2221,9 @@ int gs_er_scores(gs_ctx *c, int64_t col0, int64_t col1, int64_t e0, int64_t e1, 
         GS_CHECK(er.solved, GS_ESTATE, "gs_er_solve first");
         GS_CHECK(0 <= col0 && col0 <= col1 && col1 <= er.k, GS_EINVAL, "bad column range");
         GS_CHECK(0 <= e0 && e0 <= e1 && e1 <= c->g.nnz, GS_EINVAL, "bad edge range");
+        GS_CHECK(er_cols_solved(er, col0, col1), GS_ESTATE,
+                 "columns [%lld, %lld) were not all solved since gs_er_prepare", (long long)col0,
+                 (long long)col1);
         GS_HIP(hipSetDevice(c->device));
         int64_t cnt = e1 - e0;
         double *dout = (double *)out_device(c, c->outbuf, out, sizeof(double) * cnt, loc);
@@ -2226,6 +2246,9 @@ int gs_er_copy_z(gs_ctx *c, int64_t col0, int64_t col1, double *out, int loc) {
         GS_CHECK(er.solved, GS_ESTATE, "gs_er_solve first");
         GS_CHECK(out, GS_EINVAL, "out is NULL");
         GS_CHECK(0 <= col0 && col0 <= col1 && col1 <= er.k, GS_EINVAL, "bad column range");
+        GS_CHECK(er_cols_solved(er, col0, col1), GS_ESTATE,
+                 "columns [%lld, %lld) were not all solved since gs_er_prepare", (long long)col0,
+                 (long long)col1);
         GS_HIP(hipSetDevice(c->device));
         const int64_t nc = col1 - col0;
         if (nc && er.n)

@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <array>
 #include <cstdint>
 #include <cstdio>
@@ -130,6 +131,8 @@ struct ErState {
     int64_t proj_c0 = 0, proj_c1 = 0;  // JL columns of Y the projection fills (a rank's slice)
     std::vector<int64_t> prep_key;      // (graph epoch, k, reg) the state above was built for
     void *rr_zeroed = nullptr;          // Rr allocation whose row padding has been zeroed
+    int64_t rr_k = 0;                   // ... for this k (the padding is [k, ld) of each row)
+    std::vector<uint8_t> col_solved;    // [k] solved since the last gs_er_prepare
     // mode 4 / 5 setup read back once per (graph epoch, reg): unit-weight flags, SELL
     // entry count and slice widths (no host round trip on later solves)
     std::vector<int64_t> unit_key;

@@ -194,7 +194,7 @@ def sharded_edge_scores(engine, comm: Comm, metric: str, bounds: list[int] | Non
 
 
 def sharded_sparsify(engine, comm: Comm, scores, num_edges: int, retention_ratio: float,
-                     keep_lowest: bool = False, tie_break: str = "stable", out=None):
+                     keep_lowest: bool = False, tie_break: str | None = None, out=None):
     """GraphSparsifier.sparsify's top-k (core.py:221-242) after the score
     all-gather: every rank holds the same full score vector (sharded_*), so every
     rank selects the same global top ``int(E*r)`` -- the radix select of
@@ -202,11 +202,18 @@ def sharded_sparsify(engine, comm: Comm, scores, num_edges: int, retention_ratio
 
     tie_break "stable": the device tie rule (= np.argsort(kind='stable'));
     "numpy": an ambiguous tie block at the cut is resolved by the reference's own
-    np.argsort call on the host (small graphs; identical on every rank of a node).
+    np.argsort call on the host (identical on every rank of a node).  None (the
+    default) resolves as GraphSparsifier does: $GSPARSE_TIE_BREAK, else "numpy" --
+    so every rank keeps exactly the columns a single-GPU ``sparsify`` keeps.
     Returns (mask, info): a bool tensor on the comm device (a CPU tensor for gloo)
     and the cut / #beyond / #tied of the selection."""
     if not 0 < retention_ratio <= 1:
         raise ValueError(f"retention_ratio must be in (0, 1], got {retention_ratio}")
+    import os
+
+    tie_break = tie_break or os.environ.get("GSPARSE_TIE_BREAK", "numpy")
+    if tie_break not in ("numpy", "stable"):
+        raise ValueError(f"tie_break must be 'numpy' or 'stable', got {tie_break!r}")
     cuda = comm.device.type == "cuda"
     if retention_ratio == 1.0:
         m = torch.ones(num_edges, dtype=torch.bool, device=comm.device if cuda else "cpu")

@@ -118,21 +118,39 @@ def chung_lu(n: int = 2_708, m: int = 5_278, gamma: float = 2.5, seed: int = 0) 
     return _symmetrise(perm[np.asarray(us)], perm[np.asarray(vs)], n)
 
 
-def citation_like(n: int = 169_343, m: int = 1_160_000, seed: int = 0) -> np.ndarray:
-    """Symmetrised preferential-attachment-style graph of ogbn-arxiv size."""
+def citation_like(n: int = 169_343, m: int = 1_166_243, seed: int = 0) -> np.ndarray:
+    """Symmetrised citation graph of ogbn-arxiv size: exactly ``m`` distinct
+    citations (ogbn-arxiv: 1,166,243 directed, one per undirected pair here, so
+    2m = 2,332,486 CSR entries -- SURVEY 8(d)'s ~2.32M).
+
+    Node s cites earlier nodes only (s > t): a uniform or a degree-biased target
+    (the target of an earlier sampled citation, i.e. endpoint copying), each
+    with probability 1/2.  Citation counts per node are fractional on average
+    (m / (n - 1) = 6.89): every node cites floor(m / (n-1)), a seeded choice of
+    the others one more; citations lost to duplicates are topped up by fresh
+    draws (uniform citing node, same target rule) until exactly m remain."""
     rng = np.random.default_rng(seed)
-    # Each node cites ~m/n earlier nodes, chosen by a mix of uniform and
-    # degree-biased (via endpoint copying) selection.
-    per = max(1, m // n)
-    src = np.repeat(np.arange(1, n, dtype=np.int64), per)
-    u = rng.random(src.size)
-    dst = (u * src).astype(np.int64)  # uniform among earlier nodes
-    copy = rng.random(src.size) < 0.5
-    # degree bias: copy the target of an earlier sampled edge
-    j = (rng.random(src.size) * np.arange(src.size)).astype(np.int64)
-    dst = np.where(copy, dst[j], dst)
-    dst = np.minimum(dst, src - 1)
-    return _symmetrise(src, dst, n)
+    nodes = np.arange(1, n, dtype=np.int64)
+    base, extra = divmod(m, n - 1)
+    per = np.full(n - 1, base, dtype=np.int64)
+    per[rng.choice(n - 1, size=extra, replace=False)] += 1
+    src = np.repeat(nodes, per)
+
+    def targets(s: np.ndarray) -> np.ndarray:
+        d = (rng.random(s.size) * s).astype(np.int64)  # uniform among earlier nodes
+        copy = rng.random(s.size) < 0.5
+        j = (rng.random(s.size) * np.arange(s.size)).astype(np.int64)
+        return np.minimum(np.where(copy, d[j], d), s - 1)
+
+    keys = np.unique(src * n + targets(src))
+    while keys.size < m:
+        need = m - keys.size
+        s = rng.integers(1, n, size=2 * need + 1024, dtype=np.int64)
+        k = s * n + targets(s)
+        k = k[~np.isin(k, keys)]
+        _, first = np.unique(k, return_index=True)  # fresh keys, first draws in order
+        keys = np.union1d(keys, k[np.sort(first)[:need]])
+    return _symmetrise(keys // n, keys % n, n)
 
 
 def features(n: int, f: int, seed: int = 1, kind: str = "normal") -> np.ndarray:

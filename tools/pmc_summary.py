@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 counter-collection CSVs per kernel.
 
-usage: pmc_summary.py OUT.json DIR [DIR ...]
+usage: pmc_summary.py [--calls=N] OUT.json DIR [DIR ...]
+
+--calls=N: the profiled command made N calls of each profiled region (bench.py
+--steps S --warmup W --box-order-steps 0: N = S + W); bench.py then divides
+every kernel's launches x per-launch counters of a region by N -- exactly the
+kernels one timed call launches, each weighted by its own launch count.
 
 The summary's "_meta" records the source hash of the libgsparse sources it
 profiled (tools/provenance.py) and the git HEAD; bench.py refuses to join
@@ -30,9 +35,14 @@ def short(name: str) -> str:
 
 
 def main() -> None:
-    out = sys.argv[1]
+    argv = sys.argv[1:]
+    calls = None
+    if argv and argv[0].startswith("--calls="):
+        calls = int(argv.pop(0).split("=", 1)[1])
+    out = argv[0]
+    dirs = argv[1:]
     acc = defaultdict(lambda: defaultdict(list))
-    for d in sys.argv[2:]:
+    for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f, newline="") as fh:
                 for row in csv.DictReader(fh):
@@ -50,7 +60,9 @@ def main() -> None:
             e["L2_hit_rate"] = round(h / (h + m), 4) if h + m else None
         res[k] = e
     res["_meta"] = {"source_hash": source_hash(), "git_head": git_head(),
-                    "passes": [os.path.basename(d.rstrip("/")) for d in sys.argv[2:]]}
+                    "passes": [os.path.basename(d.rstrip("/")) for d in dirs]}
+    if calls:
+        res["_meta"]["calls_per_run"] = calls
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     for k, e in sorted(((k, e) for k, e in res.items() if k != "_meta"),
