@@ -134,14 +134,16 @@ __device__ __forceinline__ int bb_col_part(int64_t u, int64_t v, int nparts) {
 }
 
 // 2-hop witness. state: 0 = unresolved, 1 = keep, 2 = prune.
-// Only the columns of this part (bb_col_part) are decided here: the other parts'
-// columns are marked 3 and never decided by this part (k_bb_need, k_bb_keep).
+// Columns [c0, c1) only (the staged multi-rank form splits them in ranges; the rest
+// keep their state).  Pair form (nparts > 1): only the columns of this part
+// (bb_col_part) are decided here: the other parts' columns are marked 3 and never
+// decided by this part (k_bb_need, k_bb_keep).
 __global__ void k_bb_witness(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
-                             const double *__restrict__ w, int64_t E,
+                             const double *__restrict__ w, int64_t c0, int64_t c1,
                              const int64_t *__restrict__ gp, const int32_t *__restrict__ gi,
                              const double *__restrict__ gw, double eps, int part, int nparts,
                              uint8_t *__restrict__ state) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+    for (int64_t i = c0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < c1;
          i += (int64_t)gridDim.x * blockDim.x) {
         int64_t u = src[i], v = dst[i];
         if (nparts > 1 && bb_col_part(u, v, nparts) != part) {
@@ -334,8 +336,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp(
     const int64_t *__restrict__ order, const int64_t *__restrict__ dst,
     const double *__restrict__ w, double eps, uint8_t *__restrict__ state,
     unsigned long long *__restrict__ dist_all, int32_t *__restrict__ qflag_all,
-    int32_t *__restrict__ fr_all, int32_t *__restrict__ touched_all,
-    unsigned long long *__restrict__ relax_total) {
+    int32_t *__restrict__ fr_all, int32_t *__restrict__ touched_all, int64_t b0, int64_t b1,
+    int part, int nparts, unsigned long long *__restrict__ relax_total) {
     __shared__ int s_fcount, s_ncount, s_tcount;
     __shared__ double s_wmax, s_wnext;
     __shared__ unsigned long long s_relax;
@@ -346,7 +348,10 @@ __global__ void __launch_bounds__(NT) k_bb_sssp(
     int32_t *touched = touched_all + (int64_t)blockIdx.x * n;
     if (threadIdx.x == 0) s_relax = 0;
     unsigned long long relax = 0;
-    for (int64_t si = blockIdx.x; si < nsrc; si += gridDim.x) {
+    // sources [b0, b1) of the list (b1 <= nsrc), this part's every nparts-th one
+    for (int64_t j = blockIdx.x;; j += gridDim.x) {
+        const int64_t si = b0 + part + j * nparts;
+        if (si >= b1) break;
         const int64_t u = sources[si];
         const int64_t c0 = optr[u], c1 = optr[u + 1];
         if (threadIdx.x == 0) {
@@ -593,8 +598,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     int32_t *__restrict__ fr_all, uint32_t *__restrict__ fm_all, int32_t *__restrict__ touched_all,
     int32_t *__restrict__ far_all, double delta, int cross, const uint64_t *__restrict__ skeys,
     const int64_t *__restrict__ sidx, const int64_t *__restrict__ rpos, int64_t E, double mrg,
-    int rev, unsigned long long *__restrict__ batch_next,
-    unsigned long long *__restrict__ relax_total) {
+    int rev, int64_t b0, int64_t b1, int part, int nparts,
+    unsigned long long *__restrict__ batch_next, unsigned long long *__restrict__ relax_total) {
     static_assert(S >= 1 && S <= 16, "1..16 sources per workgroup");
     // queue bits of the per-node mask; the near-far order needs S more bits for the
     // far pile (S <= 8 only: 16 sources fill the word)
@@ -631,10 +636,12 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     // batches taken in order from a global counter as workgroups free up (batch_next;
     // null: static striding), so the long searches at the end of the order do not
     // leave workgroups idle behind a fixed share
+    // batches [b0, b1) of the processing order (b1 <= nbatch), this part's every
+    // nparts-th one: the j-th taken is b0 + part + j * nparts
     __shared__ long long s_bq;
     if (threadIdx.x == 0) s_bq = batch_next ? (long long)atomicAdd(batch_next, 1ull) : (long long)blockIdx.x;
     __syncthreads();
-    for (int64_t bq = s_bq; bq < nbatch; bq = s_bq) {
+    for (int64_t bj = s_bq, bq = b0 + part + bj * nparts; bq < b1; bj = s_bq, bq = b0 + part + bj * nparts) {
         // rev: the batches from the last (the sources are in node order, i.e. by
         // descending column count after the relabeling)
         const int64_t bi = rev ? nbatch - 1 - bq : bq;
@@ -1067,7 +1074,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
             qmask[y] = 0u;
         }
         if (threadIdx.x == 0)
-            s_bq = batch_next ? (long long)atomicAdd(batch_next, 1ull) : (long long)(bq + gridDim.x);
+            s_bq = batch_next ? (long long)atomicAdd(batch_next, 1ull) : (long long)(bj + gridDim.x);
         __syncthreads();
     }
     atomicAdd(&s_relax, relax);
@@ -1076,10 +1083,13 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
 }
 
 // Full searches from K landmarks: D[x*K + l] = d_fl(landmark l, x) (+inf if
-// unreachable).  One workgroup per landmark.
+// unreachable).  One workgroup per landmark; the landmarks l = lpart (mod lparts)
+// only (the staged multi-rank form splits them over the ranks; D is +inf and
+// complete 0 for the others, which the exchange's min / max fills in).
 __global__ void __launch_bounds__(1024) k_bb_landmarks(
     const int64_t *__restrict__ gp, const int32_t *__restrict__ gi, const double *__restrict__ gw,
-    int64_t n, const int32_t *__restrict__ lm, int K, int max_rounds, double *__restrict__ D,
+    int64_t n, const int32_t *__restrict__ lm, int K, int lpart, int lparts, int max_rounds,
+    double *__restrict__ D,
     int32_t *__restrict__ complete, unsigned long long *__restrict__ dist_all,
     int32_t *__restrict__ qflag_all, int32_t *__restrict__ fr_all,
     int32_t *__restrict__ touched_all) {
@@ -1091,7 +1101,7 @@ __global__ void __launch_bounds__(1024) k_bb_landmarks(
     int32_t *fb = fa + n;
     int32_t *touched = touched_all + (int64_t)blockIdx.x * n;
     unsigned long long relax = 0;
-    for (int l = blockIdx.x; l < K; l += gridDim.x) {
+    for (int l = lpart + (int)blockIdx.x * lparts; l < K; l += (int)gridDim.x * lparts) {
         if (threadIdx.x == 0) {
             s_fcount = 1;
             s_ncount = 0;
@@ -1177,12 +1187,12 @@ __global__ void __launch_bounds__(256) k_bb_pairs(
 // m = max(1e-8, 8 n 2^-53) bounds the relative rounding of folds over simple
 // paths (< n terms each, two of them per walk).
 __global__ void k_bb_certify(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
-                             const double *__restrict__ w, int64_t E,
+                             const double *__restrict__ w, int64_t c0, int64_t c1,
                              const int64_t *__restrict__ gp, const int32_t *__restrict__ gi,
                              const double *__restrict__ gw, const double *__restrict__ D,
                              const int32_t *__restrict__ complete, int K, double eps, double m,
                              uint8_t *__restrict__ state) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+    for (int64_t i = c0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < c1;
          i += (int64_t)gridDim.x * blockDim.x) {
         if (state[i] != 0) continue;  // decided, or another part's column (3)
         const int64_t u = src[i], v = dst[i];
@@ -1374,277 +1384,424 @@ static void bb_build_graph(gs_ctx *c, int64_t n, int64_t E, const int64_t *dsrc,
     exclusive_scan_i64(c, (const int64_t *)deg, gp, n + 1);
 }
 
+// ---------------------------------------------------------------------------
+// Host side, in stages (the prune over N ranks).  One call of
+// gs_metric_backbone runs them back to back; the multi-rank form
+// (gsparse.distributed.sharded_backbone) runs them on every rank with one exchange
+// between stages:
+//   begin     relabel, G, columns by row, this rank's landmark searches (l = part mod N)
+//             -> exchange D (min) and the completeness flags (max)
+//   certify   2-hop witness + degree-1 / landmark certificates of this rank's column
+//             range -> exchange the column states (max: 0 open < 1 keep < 2 prune; two
+//             ranks that decide a column decide it the same way, every rule is exact)
+//   plan      the sources with open columns (the same list on every rank)
+//   search    batches [b0, b1) of the ascending-count order, this rank's every N-th
+//             -> exchange the states; the next range starts from every rank's decisions
+//             (the short searches' reverse-column decisions close most hub columns
+//             before the hubs search)
+//   finish    keep bytes of every column
+// The legacy one-exchange form (gs_metric_backbone_part: pairs max(u, v) % N, keep
+// bytes summed) runs the same stages with the pair flags.
+namespace gs {
+struct BbRun {
+    bool begun = false, certified = false, planned = false;
+    int64_t n = 0, E = 0;
+    double eps = 0.0;
+    int pair_part = 0, pair_nparts = 1;
+    const int64_t *dsrc = nullptr, *ddst = nullptr, *osrc = nullptr, *odst = nullptr;
+    const double *dw = nullptr;
+    int64_t *gp = nullptr;
+    int32_t *gi = nullptr;
+    double *gw = nullptr;
+    double wmed = 0.0;
+    int64_t *optr = nullptr, *order = nullptr;
+    uint8_t *state = nullptr;
+    int K = 0;
+    double *D = nullptr;
+    int32_t *lcomp = nullptr;
+    std::vector<int32_t> lm_ids;  // host source of an async copy: lives with the run
+    int64_t nsrc = 0, nbatch = 0, slabs = 0;
+    int S = 1, bt = 256;
+    int64_t *sources = nullptr;
+    unsigned long long *dist = nullptr;
+    int32_t *qflag = nullptr, *fr = nullptr, *touched = nullptr, *farl = nullptr;
+    uint32_t *fm = nullptr;
+    uint64_t *skeys = nullptr;
+    int64_t *sidx = nullptr, *rpos = nullptr;
+    int cross = 1, rev = 1;
+    bool dynamic = true;
+    double delta = 0.0;
+    unsigned long long *misc = nullptr;  // [0] unique edges, [1] relaxations, [2] batch
+                                         // counter, [3] debug count; misc + 4: bad flag
+    hipEvent_t tall = nullptr;           // the "metric_backbone" profile region
+};
+}  // namespace gs
+
+static BbRun &bb_run(gs_ctx *c) {
+    if (!c->bb) c->bb = std::make_shared<BbRun>();
+    return *c->bb;
+}
+
+static void bb_begin(gs_ctx *c, int64_t n, int64_t E, const int64_t *src, const int64_t *dst,
+                     const double *w, int64_t nw, int loc, double eps, int lpart, int lparts,
+                     int pair_part, int pair_nparts) {
+    GS_CHECK(c, GS_EINVAL, "null context");
+    // the reference indexes edge_weights[idx] for every column (metric_backbone.py:73-74)
+    GS_CHECK(nw >= E, GS_EINDEX, "index %lld is out of bounds for axis 0 with size %lld",
+             (long long)nw, (long long)nw);
+    GS_CHECK(E == 0 || (src && dst && w), GS_EINVAL, "null column/weight array");
+    GS_CHECK(lparts >= 1 && 0 <= lpart && lpart < lparts, GS_EINVAL, "bad part %d of %d", lpart, lparts);
+    GS_CHECK(pair_nparts >= 1 && 0 <= pair_part && pair_part < pair_nparts, GS_EINVAL,
+             "bad part %d of %d", pair_part, pair_nparts);
+    GS_CHECK(n >= 0 && E >= 0, GS_EINVAL, "negative n/E");
+    GS_CHECK(n < (int64_t(1) << 31), GS_EUNSUPPORTED, "n >= 2^31");
+    GS_HIP(hipSetDevice(c->device));
+    BbRun &R = bb_run(c);
+    R.begun = R.certified = R.planned = false;
+    R.n = n;
+    R.E = E;
+    R.eps = eps;
+    R.pair_part = pair_part;
+    R.pair_nparts = pair_nparts;
+    R.K = 0;
+    R.nsrc = R.nbatch = 0;
+    hipStream_t s = c->stream;
+    // own buffers (the scorer scratch slots stay untouched)
+#define BB(name) DevBuf &b_##name = c->buf("bb_" #name)
+    BB(src); BB(dst); BB(w); BB(okeys); BB(order); BB(optr); BB(state); BB(flag); BB(misc);
+    BB(lm); BB(land); BB(lcomp); BB(dist); BB(qflag); BB(fr); BB(touched); BB(msrc); BB(mdst);
+    BB(perm);
+#undef BB
+    const int64_t *dsrc = (const int64_t *)to_device(c, b_src, src, sizeof(int64_t) * E, loc);
+    const int64_t *ddst = (const int64_t *)to_device(c, b_dst, dst, sizeof(int64_t) * E, loc);
+    const int64_t *osrc = dsrc, *odst = ddst;  // the caller's ids
+    bool relabel = E > 0 && n > 1;
+    if (const char *e = getenv("GSPARSE_BB_RELABEL")) relabel = relabel && atoi(e) != 0;
+    // only graphs whose ids carry no locality of their own (mean |u - v| above n / 64:
+    // R-MAT 0.33 n; a word chain with short chords ~2) -- relabeling a chain-ordered
+    // graph by degree would scatter it (Roman-like: 2.2 -> 3.2 ms)
+    if (relabel && !getenv("GSPARSE_BB_RELABEL")) {
+        unsigned long long *gs = (unsigned long long *)c->buf("bb_gap").ensure(8);
+        GS_HIP(hipMemsetAsync(gs, 0, 8, s));
+        k_bb_gap<<<grid_for(E, 256, 2048), 256, 0, s>>>(dsrc, ddst, E, gs);
+        unsigned long long hg = 0;
+        GS_HIP(hipMemcpyAsync(&hg, gs, 8, hipMemcpyDeviceToHost, s));
+        GS_HIP(hipStreamSynchronize(s));
+        relabel = (double)hg / (double)E > (double)n / 64.0;
+    }
+    if (relabel) {
+        // validate before indexing the counters with the raw ids
+        int *bad0 = (int *)c->buf("bb_bad0").ensure(sizeof(int));
+        GS_HIP(hipMemsetAsync(bad0, 0, sizeof(int), s));
+        uint64_t *k0 = (uint64_t *)c->buf("bb_keys").ensure(8 * E);
+        int64_t *i0 = (int64_t *)c->buf("bb_idx").ensure(8 * E);
+        k_bb_keys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, dsrc, ddst, (const double *)to_device(
+            c, b_w, w, sizeof(double) * E, loc), E, n, k0, i0, bad0);
+        int hb = 0;
+        GS_HIP(hipMemcpyAsync(&hb, bad0, 4, hipMemcpyDeviceToHost, s));
+        GS_HIP(hipStreamSynchronize(s));
+        GS_CHECK(!(hb & 1), GS_EINVAL, "edge_index entry out of range [0, %lld)", (long long)n);
+        auto *cnt = (unsigned long long *)b_flag.ensure(8 * (n + 1));
+        GS_HIP(hipMemsetAsync(cnt, 0, 8 * (n + 1), s));
+        k_bb_count<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, E, cnt);
+        uint64_t *nk = (uint64_t *)b_okeys.ensure(8 * (n > E ? n : E));
+        int64_t *ids = (int64_t *)b_order.ensure(8 * (n > E ? n : E));
+        k_bb_relabel_keys<<<grid_for(n, 256, 8192), 256, 0, s>>>(cnt, n, nk, ids);
+        sort_pairs_u64_i64(c, nk, ids, n, 64);
+        int64_t *perm = (int64_t *)b_perm.ensure(8 * n);
+        k_bb_perm<<<grid_for(n, 256, 8192), 256, 0, s>>>(ids, n, perm);
+        int64_t *ms = (int64_t *)b_msrc.ensure(8 * E), *md = (int64_t *)b_mdst.ensure(8 * E);
+        k_bb_map<<<grid_for(E, 256, 8192), 256, 0, s>>>(perm, dsrc, ddst, E, ms, md);
+        GS_HIP(hipGetLastError());
+        dsrc = ms;
+        ddst = md;
+    }
+    R.dsrc = dsrc;
+    R.ddst = ddst;
+    R.osrc = osrc;
+    R.odst = odst;
+    R.dw = (const double *)to_device(c, b_w, w, sizeof(double) * E, loc);
+    R.misc = (unsigned long long *)b_misc.ensure(64);
+    GS_HIP(hipMemsetAsync(R.misc, 0, 64, s));
+    R.state = (uint8_t *)b_state.ensure(E ? E : 1);
+    if (E) GS_HIP(hipMemsetAsync(R.state, 0, E, s));
+    R.tall = prof_begin(c);
+    if (E > 0) {
+        hipEvent_t t0 = prof_begin(c);  // ended as "bb_build" below (no leak at E = 0)
+        bb_build_graph(c, n, E, dsrc, ddst, osrc, odst, R.dw, R.misc, R.gp, R.gi, R.gw, &R.wmed);
+        unsigned long long *deg = (unsigned long long *)b_flag.ensure(8 * (n + 1));
+        // columns grouped by source row (stable: radix sort is stable)
+        uint64_t *okeys = (uint64_t *)b_okeys.ensure(8 * E);
+        R.order = (int64_t *)b_order.ensure(8 * E);
+        R.optr = (int64_t *)b_optr.ensure(8 * (n + 1));
+        GS_HIP(hipMemsetAsync(deg, 0, 8 * (n + 1), s));
+        k_bb_srckeys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, E, okeys, R.order, deg);
+        sort_pairs_u64_i64(c, okeys, R.order, E, bits_for_bb((uint64_t)n));
+        exclusive_scan_i64(c, (const int64_t *)deg, R.optr, n + 1);
+        prof_end(c, t0, "bb_build", 0.0);
+        hipEvent_t tp = prof_begin(c);
+        // landmark certificates (GSPARSE_BB_LANDMARKS = K, 0 = off; large graphs: 48 --
+        // with the reverse-column decisions the searches are what the certificates
+        // leave, RMAT-18 711 vs 725 ms at 16; 0: 2.17 s)
+        int K = n > 65536 ? 48 : 16;
+        if (const char *e = getenv("GSPARSE_BB_LANDMARKS")) K = atoi(e) < 0 ? 0 : atoi(e);
+        if (K > n) K = (int)n;
+        R.K = K;
+        if (K > 0) {
+            // landmarks: the K highest-degree nodes of G
+            std::vector<int64_t> hgp(n + 1);
+            GS_HIP(hipMemcpyAsync(hgp.data(), R.gp, 8 * (n + 1), hipMemcpyDeviceToHost, s));
+            GS_HIP(hipStreamSynchronize(s));
+            R.lm_ids.resize(n);
+            for (int64_t x = 0; x < n; ++x) R.lm_ids[x] = (int32_t)x;
+            std::partial_sort(R.lm_ids.begin(), R.lm_ids.begin() + K, R.lm_ids.end(),
+                              [&](int32_t p, int32_t q) {
+                                  const int64_t dp = hgp[p + 1] - hgp[p], dq = hgp[q + 1] - hgp[q];
+                                  return dp != dq ? dp > dq : p < q;
+                              });
+            int32_t *dlm = (int32_t *)b_lm.ensure(4 * K);
+            GS_HIP(hipMemcpyAsync(dlm, R.lm_ids.data(), 4 * K, hipMemcpyHostToDevice, s));
+            R.D = (double *)b_land.ensure(8 * (size_t)K * n);
+            k_bb_fill_u64<<<grid_for((int64_t)K * n, 256, 65536), 256, 0, s>>>(
+                (unsigned long long *)R.D, (int64_t)K * n, kInfBits);
+            R.lcomp = (int32_t *)b_lcomp.ensure(4 * K);
+            GS_HIP(hipMemsetAsync(R.lcomp, 0, 4 * K, s));
+            const int mine = (K - lpart + lparts - 1) / lparts;  // landmarks l = lpart (mod lparts)
+            if (mine > 0) {
+                unsigned long long *ldist = (unsigned long long *)b_dist.ensure(8 * (size_t)mine * n);
+                int32_t *lq = (int32_t *)b_qflag.ensure(4 * (size_t)mine * n);
+                int32_t *lfr = (int32_t *)b_fr.ensure(8 * (size_t)mine * n);
+                int32_t *ltouch = (int32_t *)b_touched.ensure(4 * (size_t)mine * n);
+                k_bb_fill_u64<<<grid_for((int64_t)mine * n, 256, 65536), 256, 0, s>>>(
+                    ldist, (int64_t)mine * n, kInfBits);
+                GS_HIP(hipMemsetAsync(lq, 0, 4 * (size_t)mine * n, s));
+                // one workgroup per landmark: 1,024 threads on large graphs (the K searches
+                // are the only work in flight then)
+                const unsigned lt = n > 65536 ? 1024 : 256;
+                k_bb_landmarks<<<(unsigned)mine, lt, 0, s>>>(R.gp, R.gi, R.gw, n, dlm, K, lpart, lparts,
+                                                              kBbLandmarkRounds, R.D, R.lcomp, ldist, lq,
+                                                              lfr, ltouch);
+                GS_HIP(hipGetLastError());
+            }
+        }
+        prof_end(c, tp, "bb_landmarks", 0.0);
+    }
+    R.begun = true;
+}
+
+// witness + certificates of columns [E part / nparts, E (part + 1) / nparts)
+static void bb_certify(gs_ctx *c, int part, int nparts) {
+    BbRun &R = bb_run(c);
+    GS_CHECK(R.begun, GS_ESTATE, "gs_bb_begin first");
+    GS_CHECK(nparts >= 1 && 0 <= part && part < nparts, GS_EINVAL, "bad part %d of %d", part, nparts);
+    GS_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const int64_t E = R.E, c0 = E * part / nparts, c1 = E * (part + 1) / nparts;
+    hipEvent_t tp = prof_begin(c);
+    if (c1 > c0) {
+        k_bb_witness<<<grid_for(c1 - c0, 256, 8192), 256, 0, s>>>(
+            R.dsrc, R.ddst, R.dw, c0, c1, R.gp, R.gi, R.gw, R.eps, R.pair_part, R.pair_nparts, R.state);
+        if (R.K > 0) {
+            const double mrg = std::max(1e-8, 8.0 * (double)R.n * 0x1p-53);
+            k_bb_certify<<<grid_for(c1 - c0, 256, 8192), 256, 0, s>>>(R.dsrc, R.ddst, R.dw, c0, c1, R.gp,
+                                                                       R.gi, R.gw, R.D, R.lcomp, R.K,
+                                                                       R.eps, mrg, R.state);
+        }
+        GS_HIP(hipGetLastError());
+    }
+    prof_end(c, tp, "bb_certify", 0.0);
+    R.certified = true;
+}
+
+// the sources with open columns, in node order (the same list on every rank), and the
+// search geometry
+static void bb_plan(gs_ctx *c) {
+    BbRun &R = bb_run(c);
+    GS_CHECK(R.certified, GS_ESTATE, "gs_bb_certify first");
+    GS_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const int64_t n = R.n, E = R.E;
+    R.nsrc = R.nbatch = 0;
+    if (E > 0) {
+        int64_t *flag = (int64_t *)c->buf("bb_flag").ensure(8 * (n + 1));
+        int64_t *pos = (int64_t *)c->buf("bb_pos").ensure(8 * (n + 1));
+        k_bb_need<<<grid_for(n, 256, 8192), 256, 0, s>>>(R.optr, R.order, R.state, n, flag);
+        exclusive_scan_i64(c, flag, pos, n);
+        int64_t lastp = 0, lastf = 0;
+        if (n) {
+            GS_HIP(hipMemcpyAsync(&lastp, pos + n - 1, 8, hipMemcpyDeviceToHost, s));
+            GS_HIP(hipMemcpyAsync(&lastf, flag + n - 1, 8, hipMemcpyDeviceToHost, s));
+        }
+        GS_HIP(hipStreamSynchronize(s));
+        R.nsrc = lastp + lastf;
+        if (getenv("GSPARSE_BB_DEBUG")) {
+            GS_HIP(hipMemsetAsync(R.misc + 3, 0, 8, s));
+            k_bb_count0<<<grid_for(E, 256, 4096), 256, 0, s>>>(R.state, E, R.misc + 3);
+            unsigned long long open = 0;
+            GS_HIP(hipMemcpyAsync(&open, R.misc + 3, 8, hipMemcpyDeviceToHost, s));
+            GS_HIP(hipStreamSynchronize(s));
+            fprintf(stderr, "[backbone] open before searches=%llu sources=%lld\n", open,
+                    (long long)R.nsrc);
+        }
+        if (R.nsrc > 0) {
+            R.sources = (int64_t *)c->buf("bb_sources").ensure(8 * R.nsrc);
+            k_bb_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(flag, pos, n, R.sources);
+            // large graphs (big search balls): 512 workgroups of 512 threads, two per CU
+            // (RMAT-18 with the final search: 650 vs 692 ms for 256 x 1,024; round 1's
+            // plain search preferred 256 x 1,024); small ones (many short searches):
+            // 1,024 workgroups of 256 (Roman: 2.2 vs 3.0 ms)
+            const bool big = n > 65536;
+            int64_t maxslabs = big ? 512 : 1024;
+            if (const char *e = getenv("GSPARSE_BB_SLABS")) maxslabs = atoi(e) > 0 ? atoi(e) : maxslabs;
+            // sources searched together per workgroup (k_bb_sssp_multi), 1 = alone: 8 on
+            // large graphs, with the near-far order (RMAT-18: 692 ms; 16 sources, which
+            // leave no mask bits for the far pile, 725 ms -- before the reverse-column
+            // decisions 16 led, 1.85 vs 2.15 s), alone on small ones (Roman: 2.30 ms vs
+            // 2.45 ms with 8)
+            int S = big ? 8 : 1;
+            if (const char *e = getenv("GSPARSE_BB_MULTI")) {
+                const int v = atoi(e);
+                S = v >= 16 ? 16 : v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
+            }
+            R.S = S;
+            R.nbatch = (R.nsrc + S - 1) / S;
+            int64_t slabs = R.nbatch < maxslabs ? R.nbatch : maxslabs;
+            // keep the working set of all slabs under ~48 GB (of 288)
+            const double per = S == 1 ? 24.0 : 8.0 * S + 28.0;
+            int64_t cap = (int64_t)(48e9 / (per * (double)(n ? n : 1)));
+            if (cap < 1) cap = 1;
+            if (slabs > cap) slabs = cap;
+            R.slabs = slabs;
+            R.dist = (unsigned long long *)c->buf("bb_dist").ensure(8 * (size_t)S * slabs * n);
+            R.qflag = (int32_t *)c->buf("bb_qflag").ensure(4 * slabs * n);
+            R.fr = (int32_t *)c->buf("bb_fr").ensure(8 * slabs * n);
+            R.touched = (int32_t *)c->buf("bb_touched").ensure(4 * slabs * n);
+            k_bb_fill_u64<<<grid_for((int64_t)S * slabs * n, 256, 65536), 256, 0, s>>>(
+                R.dist, (int64_t)S * slabs * n, kInfBits);
+            GS_HIP(hipMemsetAsync(R.qflag, 0, 4 * slabs * n, s));
+            R.bt = big ? 512 : 256;
+            if (const char *e = getenv("GSPARSE_BB_THREADS")) R.bt = atoi(e) == 1024 ? 1024 : atoi(e) == 512 ? 512 : 256;
+            if (S > 1) {
+                R.fm = (uint32_t *)c->buf("bb_fmask").ensure(4 * slabs * n);
+                // reverse-column decisions after every search (GSPARSE_BB_CROSS=0: off)
+                R.cross = 1;
+                if (const char *e = getenv("GSPARSE_BB_CROSS")) R.cross = atoi(e) != 0;
+                R.skeys = nullptr;
+                R.sidx = R.rpos = nullptr;
+                if (R.cross) {
+                    R.skeys = (uint64_t *)c->buf("bb_skeys").ensure(8 * E);
+                    R.sidx = (int64_t *)c->buf("bb_sidx").ensure(8 * E);
+                    R.rpos = (int64_t *)c->buf("bb_rpos").ensure(8 * E);
+                    k_bb_pairkeys<<<grid_for(E, 256, 8192), 256, 0, s>>>(R.dsrc, R.ddst, E, n, R.skeys, R.sidx);
+                    sort_pairs_u64_i64(c, R.skeys, R.sidx, E, bits_for_bb((uint64_t)n * (uint64_t)n));
+                    k_bb_revpos<<<grid_for(E, 256, 8192), 256, 0, s>>>(R.dsrc, R.ddst, E, n, R.skeys, R.rpos);
+                }
+                // sources by ascending column count (the batches from the last): the
+                // short searches first, so their reverse-column decisions close most of
+                // the hubs' targets before the hubs search (RMAT-18 1.63 -> 0.83 s;
+                // GSPARSE_BB_ORDER=desc: hubs first)
+                R.rev = 1;
+                if (const char *e = getenv("GSPARSE_BB_ORDER")) R.rev = strcmp(e, "desc") != 0;
+                // batches from a global counter (misc + 2); GSPARSE_BB_DYNAMIC=0: static striding
+                R.dynamic = true;
+                if (const char *e = getenv("GSPARSE_BB_DYNAMIC")) R.dynamic = atoi(e) != 0;
+                R.farl = (int32_t *)c->buf("bb_far").ensure(8 * slabs * n);
+                // near-far step: twice the median edge weight (GSPARSE_BB_NEARFAR = the
+                // factor, 0 = plain frontier order; RMAT-18: 1 / 2 / 4 -> 687 / 692 / 700 ms
+                // at 256 x 1,024 threads, 0 -> 723 ms)
+                double nfs = 2.0;
+                if (const char *e = getenv("GSPARSE_BB_NEARFAR")) nfs = atof(e);
+                R.delta = nfs > 0.0 && R.wmed > 0.0 ? nfs * R.wmed : 0.0;
+            }
+            GS_HIP(hipGetLastError());
+        }
+    }
+    R.planned = true;
+}
+
+// search batches [b0, b1) of the processing order, this part's every nparts-th one
+static void bb_search(gs_ctx *c, int64_t b0, int64_t b1, int part, int nparts) {
+    BbRun &R = bb_run(c);
+    GS_CHECK(R.planned, GS_ESTATE, "gs_bb_plan first");
+    GS_CHECK(nparts >= 1 && 0 <= part && part < nparts, GS_EINVAL, "bad part %d of %d", part, nparts);
+    GS_CHECK(0 <= b0 && b0 <= b1 && b1 <= R.nbatch, GS_EINVAL, "batches [%lld, %lld) outside [0, %lld)",
+             (long long)b0, (long long)b1, (long long)R.nbatch);
+    GS_HIP(hipSetDevice(c->device));
+    if (b1 - b0 <= part) return;  // none of this part's
+    hipStream_t s = c->stream;
+    const int64_t mine = (b1 - b0 - part + nparts - 1) / nparts;
+    const unsigned grid = (unsigned)std::min<int64_t>(R.slabs, mine);
+    hipEvent_t tp = prof_begin(c);
+    if (R.S == 1) {
+        auto kfn = R.bt == 1024 ? k_bb_sssp<1024> : R.bt == 512 ? k_bb_sssp<512> : k_bb_sssp<256>;
+        kfn<<<grid, R.bt, 0, s>>>(R.gp, R.gi, R.gw, R.n, R.sources, R.nsrc, R.optr, R.order, R.ddst,
+                                  R.dw, R.eps, R.state, R.dist, R.qflag, R.fr, R.touched, b0, b1, part,
+                                  nparts, R.misc + 1);
+    } else {
+        unsigned long long *bnext = R.dynamic ? R.misc + 2 : nullptr;
+        if (bnext) GS_HIP(hipMemsetAsync(bnext, 0, 8, s));
+        const double mrg = std::max(1e-8, 8.0 * (double)R.n * 0x1p-53);
+        auto *qm = (uint32_t *)R.qflag;
+#define GS_BBM(NT_, S_)                                                                          \
+    k_bb_sssp_multi<NT_, S_><<<grid, NT_, 0, s>>>(R.gp, R.gi, R.gw, R.n, R.sources, R.nsrc, R.optr, \
+                                                   R.order, R.ddst, R.dw, R.eps, R.state, R.dist,  \
+                                                   qm, R.fr, R.fm, R.touched, R.farl, R.delta,     \
+                                                   R.cross, R.skeys, R.sidx, R.rpos, R.E, mrg,     \
+                                                   R.rev, b0, b1, part, nparts, bnext, R.misc + 1)
+        const int S = R.S;
+        if (R.bt == 1024) {
+            if (S == 2) GS_BBM(1024, 2); else if (S == 4) GS_BBM(1024, 4);
+            else if (S == 8) GS_BBM(1024, 8); else GS_BBM(1024, 16);
+        } else if (R.bt == 512) {
+            if (S == 2) GS_BBM(512, 2); else if (S == 4) GS_BBM(512, 4);
+            else if (S == 8) GS_BBM(512, 8); else GS_BBM(512, 16);
+        } else {
+            if (S == 2) GS_BBM(256, 2); else if (S == 4) GS_BBM(256, 4);
+            else if (S == 8) GS_BBM(256, 8); else GS_BBM(256, 16);
+        }
+#undef GS_BBM
+    }
+    GS_HIP(hipGetLastError());
+    prof_end(c, tp, "bb_search", 0.0);
+}
+
+static void bb_finish(gs_ctx *c, uint8_t *keep, int keep_loc, int64_t *n_relax) {
+    BbRun &R = bb_run(c);
+    GS_CHECK(R.certified, GS_ESTATE, "gs_bb_certify first");
+    GS_CHECK(R.E == 0 || keep, GS_EINVAL, "null keep array");
+    GS_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const int64_t E = R.E;
+    uint8_t *dkeep = (uint8_t *)out_device(c, c->buf("bb_keep"), keep, E ? E : 1, keep_loc);
+    int64_t relax = 0;
+    if (E > 0) {
+        k_bb_keep<<<grid_for(E, 256, 8192), 256, 0, s>>>(R.state, R.dsrc, R.ddst, E, R.pair_part,
+                                                       R.pair_nparts, dkeep);
+        GS_HIP(hipGetLastError());
+        unsigned long long hr = 0;
+        GS_HIP(hipMemcpyAsync(&hr, R.misc + 1, 8, hipMemcpyDeviceToHost, s));
+        GS_HIP(hipStreamSynchronize(s));
+        relax = (int64_t)hr;
+    }
+    prof_end(c, R.tall, "metric_backbone", 12.0 * (double)relax + 9.0 * (double)E);
+    R.tall = nullptr;
+    finish_out(c, keep, dkeep, E, keep_loc);
+    if (n_relax) *n_relax = relax;
+    R.begun = R.certified = R.planned = false;
+}
+
 extern "C" int gs_metric_backbone_part(gs_ctx *c, int64_t n, int64_t E, const int64_t *src,
                                        const int64_t *dst, const double *w, int64_t nw, int loc,
                                        double eps, int part, int nparts, uint8_t *keep,
                                        int keep_loc, int64_t *n_relax) {
     return guard([&] {
         GS_CHECK(c, GS_EINVAL, "null context");
-        // the reference indexes edge_weights[idx] for every column (metric_backbone.py:73-74)
-        GS_CHECK(nw >= E, GS_EINDEX, "index %lld is out of bounds for axis 0 with size %lld",
-                 (long long)nw, (long long)nw);
-        GS_CHECK(E == 0 || (src && dst && w && keep), GS_EINVAL, "null column/weight/keep array");
-        GS_CHECK(nparts >= 1 && 0 <= part && part < nparts, GS_EINVAL, "bad part %d of %d", part,
-                 nparts);
-        GS_CHECK(n >= 0 && E >= 0, GS_EINVAL, "negative n/E");
-        GS_CHECK(n < (int64_t(1) << 31), GS_EUNSUPPORTED, "n >= 2^31");
-        GS_HIP(hipSetDevice(c->device));
-        hipStream_t s = c->stream;
-        // own buffers (the scorer scratch slots stay untouched)
-#define BB(name) DevBuf &b_##name = c->buf("bb_" #name)
-        BB(src); BB(dst); BB(w); BB(okeys); BB(order); BB(optr); BB(state); BB(flag); BB(pos); BB(sources);
-        BB(dist); BB(qflag); BB(fr); BB(touched); BB(misc); BB(keep); BB(lm); BB(land); BB(lcomp);
-        BB(msrc); BB(mdst); BB(perm);
-#undef BB
-        const int64_t *dsrc =
-            (const int64_t *)to_device(c, b_src, src, sizeof(int64_t) * E, loc);
-        const int64_t *ddst =
-            (const int64_t *)to_device(c, b_dst, dst, sizeof(int64_t) * E, loc);
-        const int64_t *osrc = dsrc, *odst = ddst;  // the caller's ids
-        bool relabel = E > 0 && n > 1;
-        if (const char *e = getenv("GSPARSE_BB_RELABEL")) relabel = relabel && atoi(e) != 0;
-        // only graphs whose ids carry no locality of their own (mean |u - v| above n / 64:
-        // R-MAT 0.33 n; a word chain with short chords ~2) -- relabeling a chain-ordered
-        // graph by degree would scatter it (Roman-like: 2.2 -> 3.2 ms)
-        if (relabel && !getenv("GSPARSE_BB_RELABEL")) {
-            unsigned long long *gs = (unsigned long long *)c->buf("bb_gap").ensure(8);
-            GS_HIP(hipMemsetAsync(gs, 0, 8, s));
-            k_bb_gap<<<grid_for(E, 256, 2048), 256, 0, s>>>(dsrc, ddst, E, gs);
-            unsigned long long hg = 0;
-            GS_HIP(hipMemcpyAsync(&hg, gs, 8, hipMemcpyDeviceToHost, s));
-            GS_HIP(hipStreamSynchronize(s));
-            relabel = (double)hg / (double)E > (double)n / 64.0;
-        }
-        if (relabel) {
-            // validate before indexing the counters with the raw ids
-            int *bad0 = (int *)c->buf("bb_bad0").ensure(sizeof(int));
-            GS_HIP(hipMemsetAsync(bad0, 0, sizeof(int), s));
-            uint64_t *k0 = (uint64_t *)c->buf("bb_keys").ensure(8 * E);
-            int64_t *i0 = (int64_t *)c->buf("bb_idx").ensure(8 * E);
-            k_bb_keys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, dsrc, ddst, (const double *)to_device(
-                c, c->buf("bb_w"), w, sizeof(double) * E, loc), E, n, k0, i0, bad0);
-            int hb = 0;
-            GS_HIP(hipMemcpyAsync(&hb, bad0, 4, hipMemcpyDeviceToHost, s));
-            GS_HIP(hipStreamSynchronize(s));
-            GS_CHECK(!(hb & 1), GS_EINVAL, "edge_index entry out of range [0, %lld)", (long long)n);
-            auto *cnt = (unsigned long long *)c->buf("bb_flag").ensure(8 * (n + 1));
-            GS_HIP(hipMemsetAsync(cnt, 0, 8 * (n + 1), s));
-            k_bb_count<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, E, cnt);
-            uint64_t *nk = (uint64_t *)c->buf("bb_okeys").ensure(8 * (n > E ? n : E));
-            int64_t *ids = (int64_t *)c->buf("bb_order").ensure(8 * (n > E ? n : E));
-            k_bb_relabel_keys<<<grid_for(n, 256, 8192), 256, 0, s>>>(cnt, n, nk, ids);
-            sort_pairs_u64_i64(c, nk, ids, n, 64);
-            int64_t *perm = (int64_t *)b_perm.ensure(8 * n);
-            k_bb_perm<<<grid_for(n, 256, 8192), 256, 0, s>>>(ids, n, perm);
-            int64_t *ms = (int64_t *)b_msrc.ensure(8 * E), *md = (int64_t *)b_mdst.ensure(8 * E);
-            k_bb_map<<<grid_for(E, 256, 8192), 256, 0, s>>>(perm, dsrc, ddst, E, ms, md);
-            GS_HIP(hipGetLastError());
-            osrc = dsrc;
-            odst = ddst;
-            dsrc = ms;
-            ddst = md;
-        }
-        const double *dw = (const double *)to_device(c, b_w, w, sizeof(double) * E, loc);
-        uint8_t *dkeep = (uint8_t *)out_device(c, b_keep, keep, E ? E : 1, keep_loc);
-        unsigned long long *misc = (unsigned long long *)b_misc.ensure(64);
-        GS_HIP(hipMemsetAsync(misc, 0, 64, s));
-        int64_t relax = 0;
-        hipEvent_t tall = prof_begin(c);
-        if (E > 0) {
-            hipEvent_t t0 = prof_begin(c);  // ended as "bb_build" below (no leak at E = 0)
-            int64_t *gp;
-            int32_t *gi;
-            double *gw;
-            double wmed = 0.0;
-            bb_build_graph(c, n, E, dsrc, ddst, osrc, odst, dw, misc, gp, gi, gw, &wmed);
-            unsigned long long *deg = (unsigned long long *)b_flag.ensure(8 * (n + 1));
-            // columns grouped by source row (stable: radix sort is stable)
-            uint64_t *okeys = (uint64_t *)b_okeys.ensure(8 * E);
-            int64_t *order = (int64_t *)b_order.ensure(8 * E);
-            int64_t *optr = (int64_t *)b_optr.ensure(8 * (n + 1));
-            GS_HIP(hipMemsetAsync(deg, 0, 8 * (n + 1), s));
-            k_bb_srckeys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, E, okeys, order, deg);
-            sort_pairs_u64_i64(c, okeys, order, E, bits_for_bb((uint64_t)n));
-            exclusive_scan_i64(c, (const int64_t *)deg, optr, n + 1);
-            // 2-hop witness
-            uint8_t *state = (uint8_t *)b_state.ensure(E);
-            prof_end(c, t0, "bb_build", 0.0);
-            hipEvent_t tp = prof_begin(c);
-            k_bb_witness<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, dw, E, gp, gi, gw, eps,
-                                                               part, nparts, state);
-            prof_end(c, tp, "bb_witness", 0.0);
-            tp = prof_begin(c);
-            // landmark / degree-1 certificates (GSPARSE_BB_LANDMARKS = K, 0 = off)
-            // (large graphs: 48 -- with the reverse-column decisions the searches are
-            // what the certificates leave, RMAT-18 711 vs 725 ms at 16; 0: 2.17 s)
-            int K = n > 65536 ? 48 : 16;
-            if (const char *e = getenv("GSPARSE_BB_LANDMARKS")) K = atoi(e) < 0 ? 0 : atoi(e);
-            if (K > n) K = (int)n;
-            // landmark ids: host source of an async copy, alive until the stream sync below
-            std::vector<int32_t> ids;
-            if (K > 0) {
-                // landmarks: the K highest-degree nodes of G
-                std::vector<int64_t> hgp(n + 1);
-                GS_HIP(hipMemcpyAsync(hgp.data(), gp, 8 * (n + 1), hipMemcpyDeviceToHost, s));
-                GS_HIP(hipStreamSynchronize(s));
-                ids.resize(n);
-                for (int64_t x = 0; x < n; ++x) ids[x] = (int32_t)x;
-                std::partial_sort(ids.begin(), ids.begin() + K, ids.end(), [&](int32_t p, int32_t q) {
-                    const int64_t dp = hgp[p + 1] - hgp[p], dq = hgp[q + 1] - hgp[q];
-                    return dp != dq ? dp > dq : p < q;
-                });
-                int32_t *dlm = (int32_t *)b_lm.ensure(4 * K);
-                GS_HIP(hipMemcpyAsync(dlm, ids.data(), 4 * K, hipMemcpyHostToDevice, s));
-                double *D = (double *)b_land.ensure(8 * (size_t)K * n);
-                k_bb_fill_u64<<<grid_for((int64_t)K * n, 256, 65536), 256, 0, s>>>(
-                    (unsigned long long *)D, (int64_t)K * n, kInfBits);
-                unsigned long long *ldist = (unsigned long long *)b_dist.ensure(8 * (size_t)K * n);
-                int32_t *lq = (int32_t *)b_qflag.ensure(4 * (size_t)K * n);
-                int32_t *lfr = (int32_t *)b_fr.ensure(8 * (size_t)K * n);
-                int32_t *ltouch = (int32_t *)b_touched.ensure(4 * (size_t)K * n);
-                k_bb_fill_u64<<<grid_for((int64_t)K * n, 256, 65536), 256, 0, s>>>(ldist, (int64_t)K * n,
-                                                                                   kInfBits);
-                GS_HIP(hipMemsetAsync(lq, 0, 4 * (size_t)K * n, s));
-                int32_t *lcomp = (int32_t *)b_lcomp.ensure(4 * K);
-                // one workgroup per landmark: 1,024 threads on large graphs (the K searches
-                // are the only work in flight then)
-                const unsigned lt = n > 65536 ? 1024 : 256;
-                k_bb_landmarks<<<(unsigned)K, lt, 0, s>>>(gp, gi, gw, n, dlm, K, kBbLandmarkRounds, D,
-                                                          lcomp, ldist, lq, lfr, ltouch);
-                const double mrg = std::max(1e-8, 8.0 * (double)n * 0x1p-53);
-                k_bb_certify<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, dw, E, gp, gi, gw, D,
-                                                                   lcomp, K, eps, mrg, state);
-                GS_HIP(hipGetLastError());
-            }
-            prof_end(c, tp, "bb_certify", 0.0);
-            tp = prof_begin(c);
-            // sources needing a search
-            int64_t *flag = (int64_t *)b_flag.ensure(8 * (n + 1));
-            int64_t *pos = (int64_t *)b_pos.ensure(8 * (n + 1));
-            k_bb_need<<<grid_for(n, 256, 8192), 256, 0, s>>>(optr, order, state, n, flag);
-            exclusive_scan_i64(c, flag, pos, n);
-            int64_t lastp = 0, lastf = 0;
-            if (n) {
-                GS_HIP(hipMemcpyAsync(&lastp, pos + n - 1, 8, hipMemcpyDeviceToHost, s));
-                GS_HIP(hipMemcpyAsync(&lastf, flag + n - 1, 8, hipMemcpyDeviceToHost, s));
-            }
-            GS_HIP(hipStreamSynchronize(s));
-            int64_t nsrc = lastp + lastf;
-            if (getenv("GSPARSE_BB_DEBUG")) {
-                k_bb_count0<<<grid_for(E, 256, 4096), 256, 0, s>>>(state, E, misc + 3);
-                unsigned long long open = 0;
-                GS_HIP(hipMemcpyAsync(&open, misc + 3, 8, hipMemcpyDeviceToHost, s));
-                GS_HIP(hipStreamSynchronize(s));
-                fprintf(stderr, "[backbone] open before searches=%llu sources=%lld\n", open,
-                        (long long)nsrc);
-            }
-            if (nsrc > 0) {
-                int64_t *sources = (int64_t *)b_sources.ensure(8 * nsrc);
-                k_bb_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(flag, pos, n, sources);
-                // large graphs (big search balls): 512 workgroups of 512 threads, two per CU
-                // (RMAT-18 with the final search: 650 vs 692 ms for 256 x 1,024; round 1's
-                // plain search preferred 256 x 1,024); small ones (many short searches):
-                // 1,024 workgroups of 256 (Roman: 2.2 vs 3.0 ms)
-                const bool big = n > 65536;
-                int64_t maxslabs = big ? 512 : 1024;
-                if (const char *e = getenv("GSPARSE_BB_SLABS")) maxslabs = atoi(e) > 0 ? atoi(e) : maxslabs;
-                // sources searched together per workgroup (k_bb_sssp_multi), 1 = alone: 8 on
-                // large graphs, with the near-far order (RMAT-18: 692 ms; 16 sources, which
-                // leave no mask bits for the far pile, 725 ms -- before the reverse-column
-                // decisions 16 led, 1.85 vs 2.15 s), alone on small ones (Roman: 2.30 ms vs
-                // 2.45 ms with 8)
-                int S = big ? 8 : 1;
-                if (const char *e = getenv("GSPARSE_BB_MULTI")) {
-                    const int v = atoi(e);
-                    S = v >= 16 ? 16 : v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
-                }
-                const int64_t nunits = (nsrc + S - 1) / S;
-                int64_t slabs = nunits < maxslabs ? nunits : maxslabs;
-                // keep the working set of all slabs under ~48 GB (of 288)
-                const double per = S == 1 ? 24.0 : 8.0 * S + 28.0;
-                int64_t cap = (int64_t)(48e9 / (per * (double)(n ? n : 1)));
-                if (cap < 1) cap = 1;
-                if (slabs > cap) slabs = cap;
-                unsigned long long *dist =
-                    (unsigned long long *)b_dist.ensure(8 * (size_t)S * slabs * n);
-                int32_t *qflag = (int32_t *)b_qflag.ensure(4 * slabs * n);
-                int32_t *fr = (int32_t *)b_fr.ensure(8 * slabs * n);
-                int32_t *touched = (int32_t *)b_touched.ensure(4 * slabs * n);
-                k_bb_fill_u64<<<grid_for((int64_t)S * slabs * n, 256, 65536), 256, 0, s>>>(
-                    dist, (int64_t)S * slabs * n, kInfBits);
-                GS_HIP(hipMemsetAsync(qflag, 0, 4 * slabs * n, s));
-                int bt = big ? 512 : 256;
-                if (const char *e = getenv("GSPARSE_BB_THREADS")) bt = atoi(e) == 1024 ? 1024 : atoi(e) == 512 ? 512 : 256;
-                if (S == 1) {
-                    auto kfn = bt == 1024 ? k_bb_sssp<1024> : bt == 512 ? k_bb_sssp<512> : k_bb_sssp<256>;
-                    kfn<<<(unsigned)slabs, bt, 0, s>>>(gp, gi, gw, n, sources, nsrc, optr, order,
-                                                       ddst, dw, eps, state, dist, qflag, fr,
-                                                       touched, misc + 1);
-                } else {
-                    uint32_t *fm = (uint32_t *)c->buf("bb_fmask").ensure(4 * slabs * n);
-                    // reverse-column decisions after every search (GSPARSE_BB_CROSS=0: off)
-                    int cross = 1;
-                    if (const char *e = getenv("GSPARSE_BB_CROSS")) cross = atoi(e) != 0;
-                    uint64_t *skeys = nullptr;
-                    int64_t *sidx = nullptr, *rpos = nullptr;
-                    if (cross) {
-                        skeys = (uint64_t *)c->buf("bb_skeys").ensure(8 * E);
-                        sidx = (int64_t *)c->buf("bb_sidx").ensure(8 * E);
-                        rpos = (int64_t *)c->buf("bb_rpos").ensure(8 * E);
-                        k_bb_pairkeys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, E, n, skeys, sidx);
-                        sort_pairs_u64_i64(c, skeys, sidx, E, bits_for_bb((uint64_t)n * (uint64_t)n));
-                        k_bb_revpos<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, ddst, E, n, skeys, rpos);
-                    }
-                    const double mrg = std::max(1e-8, 8.0 * (double)n * 0x1p-53);
-                    // sources by ascending column count (the batches from the last): the
-                    // short searches first, so their reverse-column decisions close most of
-                    // the hubs' targets before the hubs search (RMAT-18 1.63 -> 0.83 s;
-                    // GSPARSE_BB_ORDER=desc: hubs first)
-                    int rev = 1;
-                    if (const char *e = getenv("GSPARSE_BB_ORDER")) rev = strcmp(e, "desc") != 0;
-                    // batches from a global counter (misc + 2, zeroed with misc);
-                    // GSPARSE_BB_DYNAMIC=0: static striding
-                    unsigned long long *bnext = misc + 2;
-                    if (const char *e = getenv("GSPARSE_BB_DYNAMIC")) bnext = atoi(e) != 0 ? bnext : nullptr;
-                    int32_t *farl = (int32_t *)c->buf("bb_far").ensure(8 * slabs * n);
-                    auto *qm = (uint32_t *)qflag;
-                    // near-far step: twice the median edge weight (GSPARSE_BB_NEARFAR = the
-                    // factor, 0 = plain frontier order; RMAT-18: 1 / 2 / 4 -> 687 / 692 / 700 ms
-                    // at 256 x 1,024 threads, 0 -> 723 ms)
-                    double nfs = 2.0;
-                    if (const char *e = getenv("GSPARSE_BB_NEARFAR")) nfs = atof(e);
-                    const double delta = nfs > 0.0 && wmed > 0.0 ? nfs * wmed : 0.0;
-#define GS_BBM(NT_, S_)                                                                        \
-    k_bb_sssp_multi<NT_, S_><<<(unsigned)slabs, NT_, 0, s>>>(gp, gi, gw, n, sources, nsrc, optr, \
-                                                            order, ddst, dw, eps, state, dist,  \
-                                                            qm, fr, fm, touched, farl, delta, \
-                                                            cross, skeys, sidx, rpos, E, mrg, \
-                                                            rev, bnext, \
-                                                            misc + 1)
-                    if (bt == 1024) {
-                        if (S == 2) GS_BBM(1024, 2); else if (S == 4) GS_BBM(1024, 4);
-                        else if (S == 8) GS_BBM(1024, 8); else GS_BBM(1024, 16);
-                    } else if (bt == 512) {
-                        if (S == 2) GS_BBM(512, 2); else if (S == 4) GS_BBM(512, 4);
-                        else if (S == 8) GS_BBM(512, 8); else GS_BBM(512, 16);
-                    } else {
-                        if (S == 2) GS_BBM(256, 2); else if (S == 4) GS_BBM(256, 4);
-                        else if (S == 8) GS_BBM(256, 8); else GS_BBM(256, 16);
-                    }
-#undef GS_BBM
-                }
-                GS_HIP(hipGetLastError());
-            }
-            prof_end(c, tp, "bb_search", 0.0);
-            k_bb_keep<<<grid_for(E, 256, 8192), 256, 0, s>>>(state, dsrc, ddst, E, part, nparts, dkeep);
-            unsigned long long hr = 0;
-            GS_HIP(hipMemcpyAsync(&hr, misc + 1, 8, hipMemcpyDeviceToHost, s));
-            GS_HIP(hipStreamSynchronize(s));
-            relax = (int64_t)hr;
-        }
-        prof_end(c, tall, "metric_backbone", 12.0 * (double)relax + 9.0 * (double)E);
-        finish_out(c, keep, dkeep, E, keep_loc);
-        if (n_relax) *n_relax = relax;
+        GS_CHECK(E == 0 || keep, GS_EINVAL, "null column/weight/keep array");
+        bb_begin(c, n, E, src, dst, w, nw, loc, eps, 0, 1, part, nparts);
+        bb_certify(c, 0, 1);
+        bb_plan(c);
+        bb_search(c, 0, bb_run(c).nbatch, 0, 1);
+        bb_finish(c, keep, keep_loc, n_relax);
     });
 }
 
@@ -1653,6 +1810,84 @@ extern "C" int gs_metric_backbone(gs_ctx *c, int64_t n, int64_t E, const int64_t
                                   double eps, uint8_t *keep, int keep_loc, int64_t *n_relax) {
     return gs_metric_backbone_part(c, n, E, src, dst, w, nw, loc, eps, 0, 1, keep, keep_loc,
                                    n_relax);
+}
+
+extern "C" int gs_bb_begin(gs_ctx *c, int64_t n, int64_t E, const int64_t *src, const int64_t *dst,
+                           const double *w, int64_t nw, int loc, double eps, int part, int nparts,
+                           int32_t *n_landmarks) {
+    return guard([&] {
+        bb_begin(c, n, E, src, dst, w, nw, loc, eps, part, nparts, 0, 1);
+        if (n_landmarks) *n_landmarks = bb_run(c).K;
+    });
+}
+
+extern "C" int gs_bb_landmarks_io(gs_ctx *c, double *D, int32_t *complete, int loc, int dir) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        BbRun &R = bb_run(c);
+        GS_CHECK(R.begun, GS_ESTATE, "gs_bb_begin first");
+        GS_CHECK(dir == 0 || dir == 1, GS_EINVAL, "dir must be 0 (out) or 1 (in)");
+        if (R.K == 0 || R.E == 0) return;
+        GS_CHECK(D && complete, GS_EINVAL, "null landmark buffers");
+        GS_HIP(hipSetDevice(c->device));
+        const size_t nd = 8 * (size_t)R.K * R.n, nc = 4 * (size_t)R.K;
+        const hipMemcpyKind k = loc == GS_DEVICE ? hipMemcpyDeviceToDevice
+                                : dir == 0 ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice;
+        if (dir == 0) {
+            GS_HIP(hipMemcpyAsync(D, R.D, nd, k, c->stream));
+            GS_HIP(hipMemcpyAsync(complete, R.lcomp, nc, k, c->stream));
+        } else {
+            GS_HIP(hipMemcpyAsync(R.D, D, nd, k, c->stream));
+            GS_HIP(hipMemcpyAsync(R.lcomp, complete, nc, k, c->stream));
+        }
+        GS_HIP(hipStreamSynchronize(c->stream));
+    });
+}
+
+extern "C" int gs_bb_certify(gs_ctx *c, int part, int nparts) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        bb_certify(c, part, nparts);
+    });
+}
+
+extern "C" int gs_bb_state_io(gs_ctx *c, uint8_t *state, int loc, int dir) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        BbRun &R = bb_run(c);
+        GS_CHECK(R.begun, GS_ESTATE, "gs_bb_begin first");
+        GS_CHECK(dir == 0 || dir == 1, GS_EINVAL, "dir must be 0 (out) or 1 (in)");
+        if (R.E == 0) return;
+        GS_CHECK(state, GS_EINVAL, "null state buffer");
+        GS_HIP(hipSetDevice(c->device));
+        const hipMemcpyKind k = loc == GS_DEVICE ? hipMemcpyDeviceToDevice
+                                : dir == 0 ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice;
+        if (dir == 0) GS_HIP(hipMemcpyAsync(state, R.state, R.E, k, c->stream));
+        else GS_HIP(hipMemcpyAsync(R.state, state, R.E, k, c->stream));
+        GS_HIP(hipStreamSynchronize(c->stream));
+    });
+}
+
+extern "C" int gs_bb_plan(gs_ctx *c, int64_t *nbatch) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        bb_plan(c);
+        if (nbatch) *nbatch = bb_run(c).nbatch;
+    });
+}
+
+extern "C" int gs_bb_search(gs_ctx *c, int64_t b0, int64_t b1, int part, int nparts) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        bb_search(c, b0, b1, part, nparts);
+    });
+}
+
+extern "C" int gs_bb_finish(gs_ctx *c, uint8_t *keep, int keep_loc, int64_t *n_relax) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        bb_finish(c, keep, keep_loc, n_relax);
+    });
 }
 
 extern "C" int gs_pair_distances(gs_ctx *c, int64_t n, int64_t E, const int64_t *src,

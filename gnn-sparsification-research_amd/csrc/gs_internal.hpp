@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -145,6 +146,7 @@ struct ErState {
 
 struct gs_ctx;
 namespace gs {
+struct BbRun;  // the staged metric backbone's state (gs_backbone.hip)
 void project_rows(gs_ctx *c, int64_t e0, int64_t e1, const double *draw, int64_t kraw, int64_t col0,
                   int64_t col1, double sqrt_k);
 }  // namespace gs
@@ -193,6 +195,7 @@ struct gs_ctx {
     bool split_abort_pending = false;
     int split_abort_parts = 0;
     int64_t split_aborts = 0;              // aborts seen by this context
+    std::shared_ptr<gs::BbRun> bb;         // staged metric backbone (gs_bb_*)
     gs::DevBuf &buf(const char *name) { return named[name]; }
 };
 

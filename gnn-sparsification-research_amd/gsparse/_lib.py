@@ -72,6 +72,14 @@ SIGNATURES = {
                                   ctypes.POINTER(_i64)]),
     "gs_metric_backbone_part": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _i64, _int, _f64, _int,
                                        _int, _vp, _int, ctypes.POINTER(_i64)]),
+    "gs_bb_begin": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _i64, _int, _f64, _int, _int,
+                           ctypes.POINTER(_i32)]),
+    "gs_bb_landmarks_io": (_int, [_vp, _vp, _vp, _int, _int]),
+    "gs_bb_certify": (_int, [_vp, _int, _int]),
+    "gs_bb_state_io": (_int, [_vp, _vp, _int, _int]),
+    "gs_bb_plan": (_int, [_vp, ctypes.POINTER(_i64)]),
+    "gs_bb_search": (_int, [_vp, _i64, _i64, _int, _int]),
+    "gs_bb_finish": (_int, [_vp, _vp, _int, ctypes.POINTER(_i64)]),
     "gs_exact_er": (_int, [_vp, _vp, _int, ctypes.POINTER(_i32)]),
     "gs_pair_distances": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _i64, _int, _i64, _vp, _vp,
                                  _vp]),

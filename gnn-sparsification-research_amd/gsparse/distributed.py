@@ -9,9 +9,11 @@ SURVEY §8(e):
     score of both CSR entries of every pair (gs_jaccard_from_counts: the
     reference's single fp64 division) -- 2 B per directed edge on the wire
     instead of the 8 B per edge of a score all-gather.
-  * metric backbone: the columns by pair (both directions of a pair on rank
-    max(u, v) % world), one all-reduce(sum) of the uint8 keep bytes (each
-    column has one contributor).
+  * metric backbone, in stages (gs_bb_*): the landmark searches split over the
+    ranks (MIN all-reduce of their labels), the columns' witnesses and
+    certificates by range, then the searches by source -- every rank's every
+    N-th batch of each range of the ascending-count order -- with a MAX
+    all-reduce of the column-state bytes after each stage.
   * AA / degree / FeatCos (and Jaccard on explicit ranges): contiguous CSR
     edge ranges (equal counts, or equal per-edge work d_u + d_v for skewed
     graphs), then an all-gather of the fp64 scores so every rank can run the
@@ -238,21 +240,74 @@ def sharded_sparsify(engine, comm: Comm, scores, num_edges: int, retention_ratio
     return mask.view(torch.bool) if mask.dtype == torch.uint8 else mask, info
 
 
-def sharded_backbone(comm: Comm, edge_index: np.ndarray, num_nodes: int,
-                     edge_weights: np.ndarray, epsilon: float = 1e-9, mask_fn=None) -> np.ndarray:
-    """metric_backbone keep mask with the columns split over ranks by pair (both
-    directions of pair {u, v} go to rank max(u, v) % world, ids as the library
-    labels them); one all-reduce(sum) of the keep bytes -- each column is decided
-    by exactly one rank."""
-    from .metric_backbone import check_weights
+def backbone_phases(nbatch: int, world: int, fractions=None) -> list[tuple[int, int]]:
+    """Search ranges of the staged backbone: batches [b0, b1) of the ascending-count
+    order, cut at the given fractions of nbatch (default $GSPARSE_BB_PHASES, else
+    BB_PHASES), one state exchange after each.  One rank: a single range."""
+    import os
 
-    check_weights(edge_weights, np.asarray(edge_index).shape[1])
-    if mask_fn is None:
-        from .metric_backbone import backbone_mask as mask_fn
-    part = mask_fn(edge_index, num_nodes, edge_weights, epsilon, part=comm.rank,
-                   nparts=comm.world)
-    t = comm.tensor(np.ascontiguousarray(part, dtype=np.uint8))
-    return comm.all_reduce_sum(t).cpu().numpy().astype(bool)
+    if world <= 1 or nbatch == 0:
+        return [(0, nbatch)]
+    if fractions is None:
+        env = os.environ.get("GSPARSE_BB_PHASES")
+        fractions = [float(x) for x in env.split(",") if x.strip()] if env else BB_PHASES
+    cuts = sorted({int(round(f * nbatch)) for f in fractions if 0.0 < f < 1.0})
+    bounds = [0] + [c for c in cuts if 0 < c < nbatch] + [nbatch]
+    return list(zip(bounds[:-1], bounds[1:]))
+
+
+# the ascending-count order's short searches decide most hub columns (reverse columns):
+# the ranks exchange their decisions at these fractions of the batch list
+BB_PHASES = (0.5, 0.8, 0.95)
+
+
+def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
+                     epsilon: float = 1e-9, stages=None, phases=None, keep_out=None):
+    """metric_backbone keep mask over ranks (metric_backbone.py:86-111), staged
+    (include/gsparse.h gs_bb_*): every rank searches the landmarks l = rank (mod N)
+    (MIN all-reduce of the labels), certifies its column range and searches its
+    every N-th batch of each range of the ascending-count source order, with one
+    MAX all-reduce of the E column-state bytes after each stage -- so a rank's later
+    searches see every rank's earlier decisions (the short searches' reverse-column
+    decisions close most hub columns before the hubs search).  Every rank returns
+    the whole mask: a bool tensor on the comm device, or a NumPy array for gloo.
+
+    `stages`: a BackboneStages (default: one on the library's shared context), or a
+    stand-in with the same methods (the CPU tests)."""
+    from .metric_backbone import BackboneStages, check_weights
+
+    E = (edge_index.shape[1] if not isinstance(edge_index, torch.Tensor)
+         else int(edge_index.shape[1]))
+    check_weights(edge_weights, E)
+    st = stages if stages is not None else BackboneStages()
+    cuda = comm.device.type == "cuda"
+    K = st.begin(edge_index, num_nodes, edge_weights, epsilon, comm.rank, comm.world)
+    if K and comm.world > 1:
+        D = torch.empty(K * num_nodes, dtype=torch.float64, device=comm.device)
+        comp = torch.empty(K, dtype=torch.int32, device=comm.device)
+        st.landmarks_io(D, comp, out=True)
+        dist.all_reduce(D, op=dist.ReduceOp.MIN, group=comm.group)
+        dist.all_reduce(comp, op=dist.ReduceOp.MAX, group=comm.group)
+        st.landmarks_io(D, comp, out=False)
+    st.certify(comm.rank, comm.world)
+    state = torch.empty(max(E, 1), dtype=torch.uint8, device=comm.device)
+
+    def exchange():
+        if comm.world > 1 and E:
+            st.state_io(state[:E], out=True)
+            dist.all_reduce(state[:E], op=dist.ReduceOp.MAX, group=comm.group)
+            st.state_io(state[:E], out=False)
+
+    exchange()
+    nb = st.plan()
+    for b0, b1 in backbone_phases(nb, comm.world, phases):
+        st.search(b0, b1, comm.rank, comm.world)
+        exchange()
+    keep = keep_out if keep_out is not None else torch.empty(max(E, 1), dtype=torch.uint8,
+                                                           device=comm.device)
+    keep, _ = st.finish(keep)
+    keep = keep[:E]
+    return keep.view(torch.bool) if cuda else keep.numpy().astype(bool)
 
 
 def er_rank_blocks(k: int, world: int, max_depth: int = 5):

@@ -67,6 +67,78 @@ def backbone_mask(edge_index: np.ndarray, num_nodes: int, edge_weights: np.ndarr
     return (mask, relax.value) if return_relax else mask
 
 
+class BackboneStages:
+    """The staged prune on one context (gs_bb_*, include/gsparse.h): what one rank of
+    ``gsparse.distributed.sharded_backbone`` runs between its exchanges.  Array
+    arguments are NumPy arrays / CPU tensors (host) or device tensors."""
+
+    def __init__(self, ctx: Context | None = None):
+        self.ctx = _context(ctx)
+        self.n = self.E = self.K = 0
+
+    @staticmethod
+    def _p(a):
+        from ._lib import GS_DEVICE
+
+        if isinstance(a, torch.Tensor):
+            return a.data_ptr(), (GS_DEVICE if a.is_cuda else GS_HOST)
+        return ptr(a), GS_HOST
+
+    def begin(self, edge_index, num_nodes: int, edge_weights, epsilon: float, part: int,
+              nparts: int) -> int:
+        """Graph, columns by row, landmark searches l = part (mod nparts); returns K."""
+        if isinstance(edge_index, torch.Tensor) and edge_index.is_cuda:
+            src, dst = edge_index[0].contiguous(), edge_index[1].contiguous()
+            E = int(src.numel())
+        else:
+            ei = np.asarray(edge_index, dtype=np.int64)
+            E = ei.shape[1]
+            src, dst = np.ascontiguousarray(ei[0]), np.ascontiguousarray(ei[1])
+        if isinstance(edge_weights, torch.Tensor) and edge_weights.is_cuda:
+            w = edge_weights.reshape(-1)[:E].contiguous()
+        else:
+            w = np.ascontiguousarray(np.asarray(edge_weights, dtype=np.float64).reshape(-1)[:E])
+        check_weights(w, E)
+        (ps, loc), (pd, _), (pw, wloc) = self._p(src), self._p(dst), self._p(w)
+        if loc != wloc:
+            raise ValueError("edge_index and edge_weights must be on the same side")
+        self._keep_alive = (src, dst, w)
+        K = ctypes.c_int32(0)
+        self.ctx.call("gs_bb_begin", int(num_nodes), E, ps, pd, pw, len(w), loc, float(epsilon),
+                      int(part), int(nparts), ctypes.byref(K))
+        self.n, self.E, self.K = int(num_nodes), E, int(K.value)
+        return self.K
+
+    def landmarks_io(self, D, complete, out: bool):
+        (pD, loc), (pc, _) = self._p(D), self._p(complete)
+        self.ctx.call("gs_bb_landmarks_io", pD, pc, loc, 0 if out else 1)
+
+    def certify(self, part: int, nparts: int):
+        self.ctx.call("gs_bb_certify", int(part), int(nparts))
+
+    def state_io(self, state, out: bool):
+        p, loc = self._p(state)
+        self.ctx.call("gs_bb_state_io", p, loc, 0 if out else 1)
+
+    def plan(self) -> int:
+        nb = ctypes.c_int64(0)
+        self.ctx.call("gs_bb_plan", ctypes.byref(nb))
+        return int(nb.value)
+
+    def search(self, b0: int, b1: int, part: int, nparts: int):
+        self.ctx.call("gs_bb_search", int(b0), int(b1), int(part), int(nparts))
+
+    def finish(self, keep=None):
+        """Keep bytes of every column (into ``keep`` if given) and the relaxations."""
+        if keep is None:
+            keep = np.zeros(max(self.E, 1), dtype=np.uint8)
+        p, loc = self._p(keep)
+        relax = ctypes.c_int64(0)
+        self.ctx.call("gs_bb_finish", p, loc, ctypes.byref(relax))
+        self._keep_alive = None
+        return keep, relax.value
+
+
 def compute_metric_backbone(
     data: Data,
     edge_weights: NDArray[np.float64],

@@ -219,6 +219,34 @@ int gs_metric_backbone_part(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *sr
                             const int64_t *dst, const double *w, int64_t nw, int loc, double eps,
                             int part, int nparts, uint8_t *keep, int keep_loc, int64_t *n_relax);
 
+/* The metric backbone in stages, for N ranks (metric_backbone.py:86-111
+ * decided by sources split over the ranks).  Every rank calls the stages in order
+ * with its own part / nparts and exchanges between them:
+ *   gs_bb_begin        relabel, G, and the landmark searches l = part (mod nparts);
+ *                      n_landmarks = K.  Exchange: the K x n landmark labels
+ *                      (gs_bb_landmarks_io, element-wise MIN over ranks; +inf where
+ *                      another rank searched) and the K completeness flags (MAX).
+ *   gs_bb_certify      2-hop witness and certificates of this part's column range.
+ *                      Exchange: the E column states (gs_bb_state_io, element-wise
+ *                      MAX: 0 open, 1 keep, 2 prune; every rule is exact, so ranks
+ *                      that decide a column decide it alike).
+ *   gs_bb_plan         the sources with open columns (the same on every rank) and
+ *                      nbatch, the search batches in their processing order.
+ *   gs_bb_search       batches [b0, b1) (0 <= b0 <= b1 <= nbatch), this part's every
+ *                      nparts-th one; exchange the states (MAX) after each range.
+ *   gs_bb_finish       keep bytes of every column (state 1).
+ * dir 0 copies the library's buffer out to D / complete / state, 1 copies it in;
+ * loc: GS_HOST or GS_DEVICE.  With one part and one range this is gs_metric_backbone. */
+int gs_bb_begin(gs_ctx *ctx, int64_t n, int64_t E, const int64_t *src, const int64_t *dst,
+                const double *w, int64_t nw, int loc, double eps, int part, int nparts,
+                int32_t *n_landmarks);
+int gs_bb_landmarks_io(gs_ctx *ctx, double *D, int32_t *complete, int loc, int dir);
+int gs_bb_certify(gs_ctx *ctx, int part, int nparts);
+int gs_bb_state_io(gs_ctx *ctx, uint8_t *state, int loc, int dir);
+int gs_bb_plan(gs_ctx *ctx, int64_t *nbatch);
+int gs_bb_search(gs_ctx *ctx, int64_t b0, int64_t b1, int part, int nparts);
+int gs_bb_finish(gs_ctx *ctx, uint8_t *keep, int keep_loc, int64_t *n_relax);
+
 /* Exact shortest-path distances for nq node pairs (qs[q], qt[q]) (host arrays;
  * out host) in the graph metric_backbone.py:70-79 builds from the columns
  * (src, dst, w): undirected, the columns with src < dst, weight the minimum

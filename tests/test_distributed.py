@@ -93,6 +93,71 @@ class OracleEngine:
         return np.sum(diff ** 2, axis=1)
 
 
+class OracleStages:
+    """gs_bb_*'s protocol (metric_backbone.BackboneStages) with the CPU oracle as each
+    rank's compute: the landmark labels of this rank's landmarks (l = rank mod N) must
+    come back whole from the MIN / MAX exchange, certify decides every third column of
+    the rank's column range, and search decides the columns of the sources of this
+    rank's batches (every N-th of each range, the batches taken from the last as the
+    library's ascending-count order takes them).  What is tested is the exchange: the
+    stages' ranges and the all-reduces must leave every column decided, and the mask
+    equal to the reference's."""
+
+    def __init__(self, S=2):
+        self.S = S
+
+    def begin(self, ei, n, w, eps, part, nparts):
+        self.ei = np.asarray(ei, dtype=np.int64)
+        self.n, self.E = n, self.ei.shape[1]
+        self.full = O.metric_backbone(self.ei, n, w, eps)
+        self.state = np.zeros(self.E, dtype=np.uint8)
+        self.K = 3
+        self.D = np.full(self.K * n, np.inf)
+        self.comp = np.zeros(self.K, dtype=np.int32)
+        for l in range(part, self.K, nparts):
+            self.D[l::self.K] = float(l)
+            self.comp[l] = 1
+        return self.K
+
+    def landmarks_io(self, D, comp, out):
+        if out:
+            D.copy_(torch.from_numpy(self.D))
+            comp.copy_(torch.from_numpy(self.comp))
+        else:
+            self.D, self.comp = D.numpy().copy(), comp.numpy().copy()
+
+    def certify(self, part, nparts):
+        assert np.array_equal(self.D, np.tile(np.arange(self.K, dtype=np.float64), self.n))
+        assert (self.comp == 1).all()
+        c0, c1 = self.E * part // nparts, self.E * (part + 1) // nparts
+        idx = np.arange(c0, c1)
+        idx = idx[idx % 3 == 0]
+        self.state[idx] = np.where(self.full[idx], 1, 2)
+
+    def state_io(self, st, out):
+        if out:
+            st.copy_(torch.from_numpy(self.state))
+        else:
+            self.state = st.numpy().copy()
+
+    def plan(self):
+        self.sources = np.unique(self.ei[0][self.state == 0])
+        self.nbatch = (len(self.sources) + self.S - 1) // self.S
+        return self.nbatch
+
+    def search(self, b0, b1, part, nparts):
+        for bq in range(b0 + part, b1, nparts):
+            bi = self.nbatch - 1 - bq
+            for u in self.sources[bi * self.S:(bi + 1) * self.S]:
+                cols = (self.ei[0] == u) & (self.state == 0)
+                self.state[cols] = np.where(self.full[cols], 1, 2)
+
+    def finish(self, keep):
+        assert (self.state != 0).all(), int((self.state == 0).sum())
+        keep[: self.E] = torch.from_numpy((self.state == 1).astype(np.uint8))
+        return keep, 0
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -128,12 +193,12 @@ def _worker(rank, world, port, name, q):
         if "backbone_jaccard" in g:
             from gsparse.distributed import sharded_backbone
 
-            def oracle_part(ei, n, w, eps, part=0, nparts=1):
-                full = O.metric_backbone(ei, n, w, eps)
-                return full & ((ei[0] % nparts) == part)
-
             bb = sharded_backbone(comm, g["edge_index"], int(g["num_nodes"]), g["cost_jaccard"],
-                                  mask_fn=oracle_part)
+                                  stages=OracleStages())
+            # one range per batch: an exchange after every batch of N ranks
+            bb1 = sharded_backbone(comm, g["edge_index"], int(g["num_nodes"]), g["cost_jaccard"],
+                                   stages=OracleStages(S=1), phases=[i / 7 for i in range(1, 7)])
+            assert np.array_equal(bb, bb1)
         # every rank selected the same kept set
         allm = [None] * world
         dist.all_gather_object(allm, {k: v.tobytes() for k, v in masks.items()})

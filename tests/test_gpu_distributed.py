@@ -209,8 +209,17 @@ def _gloo_rank(rank, world, port, q):
         e2 = gsparse.GraphSparsifier(gsparse.Data(edge_index=torch.from_numpy(ei2), num_nodes=n2),
                                      "cuda:0")._engine
         er = sharded_approx_er(e2, comm, epsilon=0.9, max_cg_iters=60, blas_threads=8).numpy()
+        # the staged metric backbone (gs_bb_*): device compute on every rank, the
+        # landmark labels and column states exchanged over gloo between the stages
+        from gsparse.distributed import sharded_backbone
+
+        bbs = {}
+        for name, (eb, nb_) in _bb_graphs().items():
+            w = _bb_costs(eb, nb_)
+            bbs[name] = sharded_backbone(comm, eb, nb_, w)
+            bbs[name + "-8phases"] = sharded_backbone(comm, eb, nb_, w, phases=[i / 8 for i in range(1, 8)])
         if rank == 0:
-            q.put((jac, er, masks))
+            q.put((jac, er, masks, bbs))
     finally:
         dist.destroy_process_group()
 
@@ -231,7 +240,7 @@ def test_ranks_sharing_the_gpu_over_gloo(gs, world, monkeypatch):
     procs = [ctx.Process(target=_gloo_rank, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    jac, er, masks = q.get(timeout=300)
+    jac, er, masks, bbs = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -251,3 +260,76 @@ def test_ranks_sharing_the_gpu_over_gloo(gs, world, monkeypatch):
     ei2 = graphs.roman_like(n2, 17500, seed=3)
     e2 = _engine(gs, ei2, n2)
     assert bits_equal(er, e2.approx_er(epsilon=0.9, max_cg_iters=60, blas_threads=8))
+    # the staged backbone over N ranks == one GPU's mask (metric_backbone.py:86-111)
+    from gsparse.metric_backbone import backbone_mask
+
+    for name, (eb, nb_) in _bb_graphs().items():
+        ref = backbone_mask(eb, nb_, _bb_costs(eb, nb_))
+        for key in (name, name + "-8phases"):
+            assert np.array_equal(bbs[key], ref), (key, int((bbs[key] != ref).sum()))
+
+
+def _bb_graphs():
+    """The staged backbone's two search forms: the hub graph (n <= 65,536: one source
+    per workgroup) and R-MAT-17 (8 sources per workgroup, reverse-column decisions)."""
+    from gsparse import graphs
+
+    ei, n = _hub_graph()
+    return {"hub": (ei, n), "rmat17": (graphs.rmat(17, 8, seed=7), 1 << 17)}
+
+
+def _bb_costs(ei, n):
+    """_scores_to_cost(Jaccard) per edge_index column (sparsify_metric_backbone)."""
+    ip, ix, _ = O.canonical_csr(ei, n)
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(ip))
+    cost = O.scores_to_cost(O.jaccard(ip, ix), "jaccard")
+    return cost[np.searchsorted(rows * n + ix, ei[0].astype(np.int64) * n + ei[1])]
+
+
+@pytest.mark.parametrize("nparts", [2, 3, 8])
+def test_staged_backbone_parts_vs_one_gpu(gs, nparts):
+    """gs_bb_* with nparts parts, each on its own library context on the one GPU and
+    the exchanges (labels MIN, flags / states MAX) done here on the device: the mask
+    equals the single-call backbone's, under the default and a one-range schedule;
+    also the relabeled R-MAT ids and the hub graph's one-source searches."""
+    from gsparse._lib import Context
+    from gsparse.distributed import backbone_phases
+    from gsparse.metric_backbone import BackboneStages, backbone_mask
+
+    dev = torch.device("cuda", 0)
+    for name, (ei, n) in _bb_graphs().items():
+        w = _bb_costs(ei, n)
+        ref = backbone_mask(ei, n, w)
+        E = ei.shape[1]
+        for fractions in (None, []):
+            st = [BackboneStages(Context(0)) for _ in range(nparts)]
+            K = [s.begin(ei, n, w, 1e-9, r, nparts) for r, s in enumerate(st)][0]
+            if K:
+                Ds = [torch.empty(K * n, dtype=torch.float64, device=dev) for _ in st]
+                Cs = [torch.empty(K, dtype=torch.int32, device=dev) for _ in st]
+                for r, s in enumerate(st):
+                    s.landmarks_io(Ds[r], Cs[r], out=True)
+                D, C = torch.stack(Ds).min(0).values, torch.stack(Cs).max(0).values
+                for s in st:
+                    s.landmarks_io(D, C, out=False)
+            for r, s in enumerate(st):
+                s.certify(r, nparts)
+            states = [torch.empty(E, dtype=torch.uint8, device=dev) for _ in st]
+
+            def exchange():
+                for r, s in enumerate(st):
+                    s.state_io(states[r], out=True)
+                m = torch.stack(states).max(0).values
+                for s in st:
+                    s.state_io(m, out=False)
+
+            exchange()
+            nbs = [s.plan() for s in st]
+            assert len(set(nbs)) == 1
+            for b0, b1 in backbone_phases(nbs[0], nparts, fractions):
+                for r, s in enumerate(st):
+                    s.search(b0, b1, r, nparts)
+                exchange()
+            for s in st:
+                keep, _ = s.finish()
+                assert np.array_equal(keep[:E].astype(bool), ref), (name, fractions)

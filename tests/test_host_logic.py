@@ -138,7 +138,7 @@ def test_short_edge_weights_raise_index_error():
         check_weights(np.zeros(4), 5)
     ei = np.array([[0, 1, 1, 2], [1, 0, 2, 1]])
     with pytest.raises(IndexError):
-        sharded_backbone(None, ei, 3, np.ones(3), mask_fn=lambda *a, **k: None)
+        sharded_backbone(None, ei, 3, np.ones(3), stages=object())
 
 
 def test_default_device_follows_torch_current_device(monkeypatch):
