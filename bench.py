@@ -478,8 +478,10 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
     Roman-like graph; costs = _scores_to_cost(Jaccard) as
     sparsify_metric_backbone passes them (core.py:251-279).  One step = the
     whole prune (graph build, witnesses, certificates, bounded searches) on
-    device-resident columns; N > 1 splits the columns by pair (max(u, v) % N) and
-    all-reduces the keep bytes."""
+    device-resident columns; N > 1 runs the staged form (gsparse.distributed.
+    sharded_backbone): landmark searches split over the ranks, witnesses and
+    certificates by column range, searches by source in ranges of the ascending-count
+    order, with all-reduces of the labels and column states between the stages."""
     import ctypes
 
     from gsparse import graphs
@@ -506,13 +508,20 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
     keep = torch.empty(E, dtype=torch.uint8, device=dev)
     comm = Comm(device=dev) if world > 1 else None
     relax = ctypes.c_int64(0)
+    if comm is not None:
+        from gsparse.distributed import sharded_backbone
+        from gsparse.metric_backbone import BackboneStages
+
+        stages = BackboneStages(ctx)
+        ei_d = torch.stack([src, dst])
 
     def step():
-        ctx.call("gs_metric_backbone_part", n, E, src.data_ptr(), dst.data_ptr(), w.data_ptr(),
-                 w.numel(), GS_DEVICE, 1e-9, rank, world, keep.data_ptr(), GS_DEVICE,
-                 ctypes.byref(relax))
         if comm is not None:
-            return comm.all_reduce_sum(keep)
+            # staged over the ranks (gs_bb_*): landmarks split, columns by range, searches
+            # by source in ranges of the ascending-count order, state all-reduces between
+            return sharded_backbone(comm, ei_d, n, w, 1e-9, stages=stages, keep_out=keep)
+        ctx.call("gs_metric_backbone", n, E, src.data_ptr(), dst.data_ptr(), w.data_ptr(),
+                 w.numel(), GS_DEVICE, 1e-9, keep.data_ptr(), GS_DEVICE, ctypes.byref(relax))
         return keep
 
     for _ in range(args.warmup):
@@ -545,7 +554,7 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
         key = f"backbone-{args.bb_graph}" + (str(args.bb_scale) if args.bb_graph == "rmat" else "")
         roofline = make_roofline("metric_backbone", p["ms"] / p["launches"], p["bytes"] / p["launches"],
                                  p["launches"], key, world)
-        roofline["relaxations_per_launch_rank0"] = relax.value
+        roofline["relaxations_per_launch_rank0"] = relax.value if comm is None else stages.relax
     result = {
         "metric": "scored edges/sec (metric backbone)", "value": round(E * args.steps / elapsed, 1),
         "unit": "scored edges/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -553,7 +562,7 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
         "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (stand-in graph of the config's size; datasets are not downloadable here)",
         "config": {"workload": wl, "n": n, "E": E, "kept": kept,
-                   "parallelism": f"column-pairs/{world}" if world > 1 else "1 GPU",
+                   "parallelism": f"staged sources/{world}" if world > 1 else "1 GPU",
                    "graph_gen_s": round(t_gen, 2)},
         "roofline": roofline,
     }
@@ -1229,6 +1238,26 @@ def main():
     }
     if rank_ms is not None:
         result["rank_ms_per_step"] = rank_ms
+    if with_topk and world == 1 and sel_info.get("tied") is not None:
+        # secondary (not `value`): what the drop-in default tie_break="numpy" adds when the
+        # cut is ambiguous -- the scores to the host and the reference's own np.argsort
+        # (core.py:233-240) -- beside the device rule timed above
+        from gsparse.selection import numpy_topk_mask
+
+        num_keep = int(E * args.keep)
+        need = num_keep - sel_info["beyond"]
+        t1 = time.perf_counter()
+        s_host = jac_out.cpu().numpy()
+        t_d2h = time.perf_counter() - t1
+        numpy_topk_mask(s_host, E, num_keep, False)
+        t_sort = time.perf_counter() - t1 - t_d2h
+        result["dropin_numpy_tie_break"] = {
+            "ambiguous_cut": bool(0 < need < sel_info["tied"]),
+            "d2h_ms": round(t_d2h * 1e3, 1), "np_argsort_mask_ms": round(t_sort * 1e3, 1),
+            "step_ms_with_it": round(ms_per_step + (t_d2h + t_sort) * 1e3, 2),
+            "note": "secondary: GraphSparsifier.sparsify's default tie rule resolves an ambiguous "
+                    "cut with the reference's np.argsort on the host; the line's value uses the "
+                    "device rule (= np.argsort(kind='stable'))"}
     if with_er and world == 1 and args.box_order_steps > 0:
         # secondary figure (not `value`): the same step in the OpenBLAS ddot order the
         # drop-in API reproduces by default on this box (threadpoolctl's thread count:

@@ -53,6 +53,10 @@ static constexpr int kPreP = GS_KPRE_P;
 #define GS_CG_V2 1
 #endif
 // V2 p update: slots past the LDS prefix handled in groups of this many (one wait each)
+// the p update fused into the SpMV pass where the graph allows it (k_cg_regwide FUSE)
+#ifndef GS_CG_FUSE
+#define GS_CG_FUSE 1
+#endif
 #ifndef GS_PGRP
 #define GS_PGRP 4
 #endif
@@ -97,6 +101,8 @@ struct RegArgs {
     const int32_t *gate;  // optional: solve the columns only if *gate != 0 (the whole-column
                           // re-solve of a split tail whose hand-offs gave up; read once at
                           // launch, wave-uniform), else every column as usual
+    int32_t fuse;         // p update fused into the SpMV pass (k_cg_regwide FUSE; the graph
+                          // and LDS layout passed k_fuse_check)
 };
 static constexpr int kRegPartTab = 4 * kRegMaxChunks + 4;
 

@@ -67,6 +67,14 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     // count's load, convert and add) -- the same bits as the count-derived value, which
     // is checked equal at setup for the unit form
     constexpr bool V2 = GS_CG_V2 && UNIT && !SPLIT;
+    // FUSE (V2, two threads per chain: wave w owns chunk w, slot u its rows 64 u ..
+    // 64 u + 63): the p update of slot u + 1 runs in the SpMV pass, right before slot u's
+    // gathers, instead of in a pass of its own behind a barrier -- slot 0, the slots past
+    // the LDS prefix and the tail rows (every row another wave may read) are updated
+    // before the barrier.  Needs every row's entries within its own chunk's slots <= its
+    // slot + 1 or among those rows (A.fuse: checked per graph and layout, k_fuse_check)
+    constexpr bool FUSE = V2 && G == 2 && GS_CG_FUSE;
+    const bool fuse = FUSE && A.fuse != 0;
     extern __shared__ double lds[];
     const int part = SPLIT ? (int)(blockIdx.x % (unsigned)A.P) : 0;
     const int group = SPLIT ? (int)(blockIdx.x / (unsigned)A.P) : (int)blockIdx.x;
@@ -570,12 +578,22 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
 #pragma unroll
                 for (int u = 0; u < kPreP && u < R; ++u) pb4[u] = pload(u);
                 if constexpr (!SPLIT) {
+                    const uint32_t zaddr = (uint32_t)zslot * 8u, saddr = (uint32_t)(zslot + 1) * 8u;  // the scratch slot
+                    if (fuse) {
+                        // slot 0 here; slots 1 .. ulds - 1 in the SpMV pass, the rest below
+                        if (0 < ulds) {
+                            const double po = lds_at(lds0());
+                            const double t1 = alpha_prev * po;
+                            x[0] = x[0] + t1;
+                            const double pb = po * beta;
+                            lds_put(valid(0) ? lds0() : saddr, pb + r[0]);
+                        }
+                    } else {
                     // two straight-line passes: every slot reads p_old from LDS (slots past
                     // the wave's LDS prefix read the zero slot and store to the scratch
                     // slot: x += alpha * 0 and p to scratch change nothing), then the slots
                     // past the prefix redo their update from the global p rows.  No branch
                     // between a prefetch and its use, so the waits count only what is needed.
-                    const uint32_t zaddr = (uint32_t)zslot * 8u, saddr = (uint32_t)(zslot + 1) * 8u;  // the scratch slot
                     double pf[R];
 #pragma unroll
                     for (int u = 0; u < kPreP && u < R; ++u) pf[u] = lds_at(u < ulds ? lds0() + 256u * G * u : zaddr);
@@ -592,6 +610,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                         const double pb = po * beta;
                         lds_put(u < ulds && valid(u) ? lds0() + 256u * G * u : saddr, pb + r[u]);
                         __builtin_amdgcn_sched_barrier(0);
+                    }
                     }
                     launder();
                     if constexpr (V2 && GS_PGRP > 0) {
@@ -701,6 +720,21 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                         eb[u + kPre] = ell_row(u + kPre);
                         if constexpr (V2) db[u + kPre] = diag_row(u + kPre);
                         else lb[u + kPre] = len_row(u + kPre);
+                    }
+                    if constexpr (FUSE) {
+                        if (u + 1 < R) {
+                            // fused p update of slot u + 1 (LDS prefix): its rows are read by
+                            // slot u's gathers (and later ones), all in this wave; a wave's
+                            // LDS operations complete in order
+                            if (fuse && it > 0 && u + 1 < ulds) {
+                                const uint32_t pa = lds0() + 256u * G * (u + 1);
+                                const double po = lds_at(pa);
+                                const double t1 = alpha_prev * po;
+                                x[u + 1] = x[u + 1] + t1;
+                                const double pb = po * beta;
+                                lds_put(valid(u + 1) ? pa : (uint32_t)(zslot + 1) * 8u, pb + r[u + 1]);
+                            }
+                        }
                     }
                     double pv = 0.0, qv = 0.0;
                     if constexpr (V2) {

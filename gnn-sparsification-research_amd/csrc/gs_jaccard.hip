@@ -20,6 +20,8 @@
 // so the output is bit-identical to the per-entry kernel in gs_scores.hip.
 #include "gs_internal.hpp"
 
+#include <type_traits>
+
 #include <vector>
 
 namespace gs {
@@ -407,35 +409,58 @@ __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
     static_assert(UL % UP == 0, "probe groups split the loaded elements");
     static_assert(64 * UL <= kIxPad, "unconditional list steps stay inside the index padding");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    using gi32 = __attribute__((address_space(1))) const int32_t;  // global, not flat
+    // one step: U list elements per lane loaded (all in flight before the first probe),
+    // lanes past d_v masked (MASK), then probed in groups of min(UP, U)
+    auto step = [&](auto Uc, auto MASKc, gi32 *lp, int32_t left, int64_t &cnt) {
+        constexpr int U = decltype(Uc)::value;
+        constexpr bool MASK = decltype(MASKc)::value;
+        constexpr int P = UP < U ? UP : U;
+        int32_t xs[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) xs[t] = lp[t * 64];
+        if constexpr (MASK) {
+#pragma unroll
+            for (int t = 0; t < U; ++t) xs[t] = lane + t * 64 < left ? xs[t] : -1;
+        }
+#pragma unroll
+        for (int g = 0; g < U; g += P) {
+            typename Probe::S ps[P];
+#pragma unroll
+            for (int t = 0; t < P; ++t) ps[t] = pr.first(xs[g + t] >= 0 ? xs[g + t] : 0);
+#pragma unroll
+            for (int t = 0; t < P; ++t) {
+                const bool hit = xs[g + t] >= 0 && pr.done(xs[g + t], ps[t]);
+                cnt += __popcll(__ballot(hit));
+            }
+        }
+    };
+    using T1 = std::true_type;
+    using F0 = std::false_type;
     for (int k = wave; k < st.nbig; k += nw) {
         const int32_t dv = __builtin_amdgcn_readfirstlane(st.dv[k]);
         // the list's base is wave-uniform: loads from a scalar base, one lane offset and
-        // immediate step offsets, unconditional -- the ones past d_v read the next rows'
-        // entries (or the kIxPad padding after the last row) and are masked
+        // immediate step offsets.  Whole 64 UL-element steps first (no mask), then one
+        // step of the fewest loads (1, 2, 4 .. UL per lane) that covers the rest, its
+        // lanes past d_v masked -- they read at most 63 entries past the list (the next
+        // rows', or the kIxPad padding after the last row).  (Round 4 read every list in
+        // 64 UL-element steps: up to 511 entries past a short list, 98 GB fetched per
+        // R-MAT-22 call against ~50 GB probed.)
         const uint64_t lb = (uint64_t)(ix + st.b[k]);
-        using gi32 = __attribute__((address_space(1))) const int32_t;  // global, not flat
         gi32 *lst = (gi32 *)(
             (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lb) |
             (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lb >> 32)) << 32);
         int64_t cnt = 0;
-        for (int32_t j0 = 0; j0 < dv; j0 += 64 * UL) {
-            int32_t xs[UL];  // all loads in flight before the first probe
-            gi32 *lp = lst + (uint32_t)(j0 + lane);
-#pragma unroll
-            for (int t = 0; t < UL; ++t) xs[t] = lp[t * 64];
-#pragma unroll
-            for (int t = 0; t < UL; ++t) xs[t] = lane + t * 64 < dv - j0 ? xs[t] : -1;
-#pragma unroll
-            for (int g = 0; g < UL; g += UP) {
-                typename Probe::S ps[UP];
-#pragma unroll
-                for (int t = 0; t < UP; ++t) ps[t] = pr.first(xs[g + t] >= 0 ? xs[g + t] : 0);
-#pragma unroll
-                for (int t = 0; t < UP; ++t) {
-                    const bool hit = xs[g + t] >= 0 && pr.done(xs[g + t], ps[t]);
-                    cnt += __popcll(__ballot(hit));
-                }
-            }
+        int32_t j0 = 0;
+        for (; j0 + 64 * UL <= dv; j0 += 64 * UL)
+            step(std::integral_constant<int, UL>{}, F0{}, lst + (uint32_t)(j0 + lane), 64 * UL, cnt);
+        const int32_t rem = dv - j0;  // wave-uniform
+        gi32 *lp = lst + (uint32_t)(j0 + lane);
+        if (rem > 0) {
+            if (rem <= 64) step(std::integral_constant<int, 1>{}, T1{}, lp, rem, cnt);
+            else if (UL >= 2 && rem <= 128) step(std::integral_constant<int, (UL >= 2 ? 2 : 1)>{}, T1{}, lp, rem, cnt);
+            else if (UL >= 4 && rem <= 256) step(std::integral_constant<int, (UL >= 4 ? 4 : 1)>{}, T1{}, lp, rem, cnt);
+            else step(std::integral_constant<int, UL>{}, T1{}, lp, rem, cnt);
         }
         if (lane == 0) sk.put(lo + st.off[k], cnt, du, dv);
     }

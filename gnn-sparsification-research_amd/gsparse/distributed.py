@@ -270,7 +270,8 @@ def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
     MAX all-reduce of the E column-state bytes after each stage -- so a rank's later
     searches see every rank's earlier decisions (the short searches' reverse-column
     decisions close most hub columns before the hubs search).  Every rank returns
-    the whole mask: a bool tensor on the comm device, or a NumPy array for gloo.
+    the whole mask as a NumPy bool array, or fills `keep_out` (uint8, E entries, on
+    the comm device) and returns it.
 
     `stages`: a BackboneStages (default: one on the library's shared context), or a
     stand-in with the same methods (the CPU tests)."""
@@ -280,7 +281,6 @@ def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
          else int(edge_index.shape[1]))
     check_weights(edge_weights, E)
     st = stages if stages is not None else BackboneStages()
-    cuda = comm.device.type == "cuda"
     K = st.begin(edge_index, num_nodes, edge_weights, epsilon, comm.rank, comm.world)
     if K and comm.world > 1:
         D = torch.empty(K * num_nodes, dtype=torch.float64, device=comm.device)
@@ -305,9 +305,10 @@ def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
         exchange()
     keep = keep_out if keep_out is not None else torch.empty(max(E, 1), dtype=torch.uint8,
                                                            device=comm.device)
-    keep, _ = st.finish(keep)
-    keep = keep[:E]
-    return keep.view(torch.bool) if cuda else keep.numpy().astype(bool)
+    st.finish(keep)
+    if keep_out is not None:  # the caller's uint8 tensor, filled in place (bench: on the device)
+        return keep_out
+    return keep[:E].cpu().numpy().astype(bool)
 
 
 def er_rank_blocks(k: int, world: int, max_depth: int = 5):

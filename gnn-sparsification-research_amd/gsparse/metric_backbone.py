@@ -136,6 +136,7 @@ class BackboneStages:
         relax = ctypes.c_int64(0)
         self.ctx.call("gs_bb_finish", p, loc, ctypes.byref(relax))
         self._keep_alive = None
+        self.relax = relax.value
         return keep, relax.value
 
 
