@@ -376,6 +376,7 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
         if (W <= 0) return;
         if (NT == 512) {
             if (G == 1) regwide_launch_g1(A, rsel, ufast, dyn, (unsigned)wslots, s);
+            else if (G == 2 && ufast && A.fuse) regwide_launch_fused_g2(A, rsel, dyn, (unsigned)wslots, s);
             else if (G == 2) regwide_launch_g2(A, rsel, ufast, dyn, (unsigned)wslots, s);
             else if (G == 4) regwide_launch_g4(A, rsel, ufast, dyn, (unsigned)wslots, s);
             else regwide_launch_g8(A, rsel, ufast, dyn, (unsigned)wslots, s);
@@ -484,6 +485,7 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     Cw.gate = B.abortf;
     const int64_t ts = std::min<int64_t>(tailn, wslots > 1 ? wslots : slots);
     if (G == 1) regwide_launch_g1(Cw, rsel, ufast, dyn, (unsigned)ts, s);
+    else if (G == 2 && ufast && Cw.fuse) regwide_launch_fused_g2(Cw, rsel, dyn, (unsigned)ts, s);
     else if (G == 2) regwide_launch_g2(Cw, rsel, ufast, dyn, (unsigned)ts, s);
     else if (G == 4) regwide_launch_g4(Cw, rsel, ufast, dyn, (unsigned)ts, s);
     else regwide_launch_g8(Cw, rsel, ufast, dyn, (unsigned)ts, s);

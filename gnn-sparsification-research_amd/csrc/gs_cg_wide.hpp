@@ -57,7 +57,7 @@ __device__ __forceinline__ double wide_readlane(double v, int ln) {
 // drained-sc1 recipe: sc1 payload, s_waitcnt vmcnt(0), barrier, one sc1 flag store, sc1
 // polls.  The chunk dots are added in global chunk order, so the bits are those of
 // the one-workgroup solve.  Used for the last, partly occupied round of columns.
-template <int G, int R, bool UNIT, bool QR, bool SPLIT = false>
+template <int G, int R, bool UNIT, bool QR, bool SPLIT = false, bool FUSED = false>
 __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     constexpr int CW = 64 / G;  // chains per wave
     // V2 (whole columns, unit weights): each slot's "any p code global" and "any row
@@ -72,9 +72,10 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     // gathers, instead of in a pass of its own behind a barrier -- slot 0, the slots past
     // the LDS prefix and the tail rows (every row another wave may read) are updated
     // before the barrier.  Needs every row's entries within its own chunk's slots <= its
-    // slot + 1 or among those rows (A.fuse: checked per graph and layout, k_fuse_check)
-    constexpr bool FUSE = V2 && G == 2 && GS_CG_FUSE;
-    const bool fuse = FUSE && A.fuse != 0;
+    // slot + 1 or among those rows (the host launches this form when k_fuse_check passed)
+    // (a compile-time form: a runtime switch between the two prologues costs ~250 VGPR
+    // spills in this kernel)
+    constexpr bool FUSE = FUSED && V2 && G == 2;
     extern __shared__ double lds[];
     const int part = SPLIT ? (int)(blockIdx.x % (unsigned)A.P) : 0;
     const int group = SPLIT ? (int)(blockIdx.x / (unsigned)A.P) : (int)blockIdx.x;
@@ -579,7 +580,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                 for (int u = 0; u < kPreP && u < R; ++u) pb4[u] = pload(u);
                 if constexpr (!SPLIT) {
                     const uint32_t zaddr = (uint32_t)zslot * 8u, saddr = (uint32_t)(zslot + 1) * 8u;  // the scratch slot
-                    if (fuse) {
+                    if constexpr (FUSE) {
                         // slot 0 here; slots 1 .. ulds - 1 in the SpMV pass, the rest below
                         if (0 < ulds) {
                             const double po = lds_at(lds0());
@@ -726,13 +727,17 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                             // fused p update of slot u + 1 (LDS prefix): its rows are read by
                             // slot u's gathers (and later ones), all in this wave; a wave's
                             // LDS operations complete in order
-                            if (fuse && it > 0 && u + 1 < ulds) {
+                            if (u + 1 < ulds) {  // wave-uniform: the slot is in the LDS prefix
+                                // iteration 0 stores p = r (as SciPy's p = z.copy()) and leaves x
+                                const bool up = it > 0;  // wave-uniform
                                 const uint32_t pa = lds0() + 256u * G * (u + 1);
-                                const double po = lds_at(pa);
+                                const double po = lds_at(up ? pa : (uint32_t)zslot * 8u);
                                 const double t1 = alpha_prev * po;
-                                x[u + 1] = x[u + 1] + t1;
+                                const double xn = x[u + 1] + t1;
+                                x[u + 1] = up ? xn : x[u + 1];
                                 const double pb = po * beta;
-                                lds_put(valid(u + 1) ? pa : (uint32_t)(zslot + 1) * 8u, pb + r[u + 1]);
+                                const double pn = pb + r[u + 1];
+                                lds_put(valid(u + 1) ? pa : (uint32_t)(zslot + 1) * 8u, up ? pn : r[u + 1]);
                             }
                         }
                     }
@@ -897,6 +902,22 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         };                                                                                    \
         (void)A.qreg; /* whole columns keep x in registers (the q-in-registers form of */     \
         pick(std::false_type{}); /* round 2 lives on only in the split tail) */               \
+    }
+
+// one launch of the fused form (two threads per chain, unit weights, x in registers):
+// the p update inside the SpMV pass (A.fuse: the graph passed k_fuse_check)
+#define GS_REGWIDE_FUSED_DEF(G_)                                                              \
+    void regwide_launch_fused_g##G_(const RegArgs &A, int R, size_t dyn, unsigned slots,     \
+                                    hipStream_t s) {                                          \
+        auto go = [&](auto kern) {                                                            \
+            GS_HIP(hipFuncSetAttribute((const void *)kern,                                    \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn)); \
+            kern<<<slots, kRegThreads, dyn, s>>>(A);                                          \
+        };                                                                                    \
+        if (R == 16) go(k_cg_regwide<G_, 16, true, false, false, true>);                      \
+        else if (R == 24) go(k_cg_regwide<G_, 24, true, false, false, true>);                 \
+        else if (R == 32) go(k_cg_regwide<G_, 32, true, false, false, true>);                 \
+        else go(k_cg_regwide<G_, 44, true, false, false, true>);                              \
     }
 
 // one launch of the split form (q in registers), grid = groups x A.P workgroups

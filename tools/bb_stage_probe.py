@@ -136,4 +136,20 @@ for fr in schedules:
                           "speedup": round(base_ms / tot, 2),
                           "stages_ms": {k: round(v, 2) for k, v in slow.items()},
                           "parts_ms": allms, "relaxations": rel}), flush=True)
+# search-geometry variants at N > 1 (argv[3]: ';'-separated "S:threads:slabs" triples;
+# GSPARSE_BB_MULTI / _THREADS / _SLABS are read at plan time, per call)
+variants = [v.split(":") for v in (sys.argv[3].split(";") if len(sys.argv) > 3 else []) if v]
+for S, th, sl in variants:
+    os.environ["GSPARSE_BB_MULTI"], os.environ["GSPARSE_BB_THREADS"] = S, th
+    os.environ["GSPARSE_BB_SLABS"] = sl
+    for N in (1, 4, 8):
+        for fr in schedules[:1]:
+            mask, slow, allms, rel, nb = run(N, fr)
+            assert torch.equal(mask, whole), (S, th, sl, fr, N)
+            tot = sum(slow.values())
+            summary[f"S{S}/t{th}/slabs{sl} {','.join(map(str, fr))}@N={N}"] = round(tot, 2)
+            print(json.dumps({"S": S, "threads": th, "slabs": sl, "phases": fr, "N": N,
+                              "rank_ms": round(tot, 2),
+                              "stages_ms": {k: round(v, 2) for k, v in slow.items()},
+                              "relaxations": sum(rel), "nbatch": nb}), flush=True)
 print(json.dumps({"summary": summary}), flush=True)

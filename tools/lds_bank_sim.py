@@ -83,6 +83,33 @@ def slot_of(x, row_owner, layout):
     raise ValueError(layout)
 
 
+DIAG = os.environ.get("DIAG", "cur")
+
+
+def diag_slot(r):
+    """cur: zs + 2 + tid (the kernel); an integer s: a slot in a separate region whose
+    bank is the own row's p bank + s (mod 32), one slot per row (a dense remap)."""
+    if DIAG == "cur":
+        return zs + 2 + owner_tid(r)
+    t = max(i for i in range(T) if r >= ca[i])
+    o = r - ca[t]
+    own = int(lbase[t]) + o
+    base = (zs + 2048) // 32 * 32 + 32
+    return base + (owner_tid(r) // 32) * 32 + ((own + int(DIAG)) % 32)
+
+
+ZERO = os.environ.get("ZERO", "cur")
+
+
+def zero_slot(r):
+    """cur: the one zero slot; an integer s: one of 32 zero slots, bank = own p bank + s."""
+    if ZERO == "cur":
+        return zs
+    t = max(i for i in range(T) if r >= ca[i])
+    own = int(lbase[t]) + r - ca[t]
+    return (zs + 8192) // 32 * 32 + ((own + int(ZERO)) % 32)
+
+
 def sim(layout):
     cycles = extra = insts = 0
     for t in range(T):
@@ -100,13 +127,13 @@ def sim(layout):
                         if k < len(lst):
                             c = lst[k]
                             if c == r:
-                                a_ = zs + 2 + owner_tid(r)
+                                a_ = diag_slot(r)
                             else:
                                 a_ = slot_of(c, r, layout)
                                 if a_ is None:
                                     a_ = 1 << 20  # global: read past the LDS (its own "bank")
                         else:
-                            a_ = zs
+                            a_ = zero_slot(r)
                         addrs.append(a_)
                     if not addrs:
                         continue
