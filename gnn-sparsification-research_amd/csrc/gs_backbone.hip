@@ -1408,6 +1408,7 @@ struct BbRun {
     int64_t n = 0, E = 0;
     double eps = 0.0;
     int pair_part = 0, pair_nparts = 1;
+    int nranks = 1;  // ranks of the staged form (the search geometry depends on it)
     const int64_t *dsrc = nullptr, *ddst = nullptr, *osrc = nullptr, *odst = nullptr;
     const double *dw = nullptr;
     int64_t *gp = nullptr;
@@ -1463,6 +1464,7 @@ static void bb_begin(gs_ctx *c, int64_t n, int64_t E, const int64_t *src, const 
     R.eps = eps;
     R.pair_part = pair_part;
     R.pair_nparts = pair_nparts;
+    R.nranks = lparts;
     R.K = 0;
     R.nsrc = R.nbatch = 0;
     hipStream_t s = c->stream;
@@ -1651,14 +1653,19 @@ static void bb_plan(gs_ctx *c) {
             // plain search preferred 256 x 1,024); small ones (many short searches):
             // 1,024 workgroups of 256 (Roman: 2.2 vs 3.0 ms)
             const bool big = n > 65536;
-            int64_t maxslabs = big ? 512 : 1024;
+            // a rank of 4 or more (staged form) has few batches per workgroup and waits on
+            // single searches: 2 sources per workgroup of 1,024 threads, 256 workgroups
+            // (RMAT-18 at N = 8: 202 ms per rank vs 258 ms with one GPU's geometry, which
+            // takes 738 vs 639 ms whole; tools/bb_stage_probe.py, profiles/r05d_*)
+            const bool wide = big && R.nranks >= 4;
+            int64_t maxslabs = big ? (wide ? 256 : 512) : 1024;
             if (const char *e = getenv("GSPARSE_BB_SLABS")) maxslabs = atoi(e) > 0 ? atoi(e) : maxslabs;
             // sources searched together per workgroup (k_bb_sssp_multi), 1 = alone: 8 on
             // large graphs, with the near-far order (RMAT-18: 692 ms; 16 sources, which
             // leave no mask bits for the far pile, 725 ms -- before the reverse-column
             // decisions 16 led, 1.85 vs 2.15 s), alone on small ones (Roman: 2.30 ms vs
             // 2.45 ms with 8)
-            int S = big ? 8 : 1;
+            int S = big ? (wide ? 2 : 8) : 1;
             if (const char *e = getenv("GSPARSE_BB_MULTI")) {
                 const int v = atoi(e);
                 S = v >= 16 ? 16 : v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
@@ -1679,7 +1686,7 @@ static void bb_plan(gs_ctx *c) {
             k_bb_fill_u64<<<grid_for((int64_t)S * slabs * n, 256, 65536), 256, 0, s>>>(
                 R.dist, (int64_t)S * slabs * n, kInfBits);
             GS_HIP(hipMemsetAsync(R.qflag, 0, 4 * slabs * n, s));
-            R.bt = big ? 512 : 256;
+            R.bt = big ? (wide ? 1024 : 512) : 256;
             if (const char *e = getenv("GSPARSE_BB_THREADS")) R.bt = atoi(e) == 1024 ? 1024 : atoi(e) == 512 ? 512 : 256;
             if (S > 1) {
                 R.fm = (uint32_t *)c->buf("bb_fmask").ensure(4 * slabs * n);

@@ -77,40 +77,6 @@ __global__ void k_ell8_fill(int32_t r0, int32_t n, int T, const int64_t *__restr
     }
 }
 
-// k_cg_regwide's FUSE condition (two threads per chain: slot u of chunk t = its rows
-// 64 u .. 64 u + 63): a row is a "prologue" row when it is in slot 0, in a slot past the
-// chunk's common LDS prefix (ulds[t] slots) or a tail row -- updated before the SpMV
-// pass's barrier; every other row of slot s is updated in the SpMV pass just before
-// slot s - 1's gathers.  So every entry c of row i must be a prologue row or a row of
-// i's chunk in a slot <= slot(i) + 1 (any slot for a tail row i).  bad[0] = 1 otherwise.
-__global__ void k_fuse_check(int32_t n, int T, const int64_t *__restrict__ tab,
-                             const int32_t *__restrict__ ulds, const int64_t *__restrict__ lp,
-                             const int32_t *__restrict__ li, int32_t *__restrict__ bad) {
-    auto chunk_of = [&](int64_t c) {
-        int t = 0;
-        while (t + 1 < T && c >= tab[t + 1]) ++t;
-        return t;
-    };
-    auto prologue = [&](int t, int64_t o) {
-        const int64_t n32 = tab[kRegMaxChunks + t] & ~(int64_t)31;
-        return o >= n32 || (o >> 6) == 0 || (o >> 6) >= ulds[t];
-    };
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int t = chunk_of(i);
-        const int64_t o = i - tab[t], n32 = tab[kRegMaxChunks + t] & ~(int64_t)31;
-        const bool tail = o >= n32;
-        bool ok = true;
-        for (int64_t e = lp[i]; e < lp[i + 1] && ok; ++e) {
-            const int64_t c = li[e];
-            const int tc = chunk_of(c);
-            const int64_t oc = c - tab[tc];
-            ok = prologue(tc, oc) || (tc == t && (tail || (oc >> 6) <= (o >> 6) + 1));
-        }
-        if (!ok) atomicOr(bad, 1);
-    }
-}
-
 // threads per chain for T chunks on an NT-thread workgroup (power of two, 32 T G <= NT,
 // G <= 8) and register row slots per thread (the chain rows); -1 when it does not apply
 static int reg_geometry(int NT, int T, const int64_t *len, int &G) {
@@ -246,28 +212,6 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
                                                           ufast ? (int32_t)zs + 2 : -1, lp, li, lv, optr,
                                                           ell, ellv, ocol, oval, rflag);
         GS_HIP(hipGetLastError());
-        // k_cg_regwide's fused p update (512 threads, two per chain, unit form): each
-        // chunk's common LDS prefix in wave-slots of 64 rows as the kernel derives it (the
-        // least over its lanes o0 = 0 .. 63 of ceil((keep - o0) / 64)), then the graph check
-        c->reg_fuse = 0;
-        if (NT == 512 && G == 2 && ufast) {
-            std::vector<int32_t> hul(kRegMaxChunks, 0);
-            for (int t = 0; t < T; ++t) {
-                int64_t m = INT64_MAX;
-                for (int64_t o0 = 0; o0 < 64; ++o0)
-                    m = std::min<int64_t>(m, keep[t] > o0 ? (keep[t] - o0 + 63) / 64 : 0);
-                hul[t] = (int32_t)m;
-            }
-            auto *dul = (int32_t *)c->buf("er_reg_fuse_ulds").ensure(sizeof(int32_t) * (kRegMaxChunks + 1));
-            GS_HIP(hipMemcpyAsync(dul, hul.data(), sizeof(int32_t) * kRegMaxChunks, hipMemcpyHostToDevice, s));
-            GS_HIP(hipMemsetAsync(dul + kRegMaxChunks, 0, sizeof(int32_t), s));
-            k_fuse_check<<<grid_for(n, 256, 8192), 256, 0, s>>>((int32_t)n, T, dch, dul, lp, li, dul + kRegMaxChunks);
-            GS_HIP(hipGetLastError());
-            int32_t hbad = 1;
-            GS_HIP(hipMemcpyAsync(&hbad, dul + kRegMaxChunks, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-            GS_HIP(hipStreamSynchronize(s));
-            c->reg_fuse = hbad == 0 ? 1 : 0;
-        }
         c->reg_ell_key = key;
     }
     RegArgs A{};
@@ -356,9 +300,6 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     A.oval = oval;
     A.diag = diag;  // L_reg's diagonal (k_l_unit), read by the whole-column unit form
     A.rflag = rflag;
-    // the p update fused into the SpMV pass (k_cg_regwide FUSE; GSPARSE_REG_FUSE=0: off)
-    A.fuse = c->reg_fuse;
-    if (const char *e = getenv("GSPARSE_REG_FUSE")) A.fuse = A.fuse && atoi(e) != 0;
 
     A.zslot = (int32_t)pad;
     A.maxiter = maxiter;
@@ -376,7 +317,6 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
         if (W <= 0) return;
         if (NT == 512) {
             if (G == 1) regwide_launch_g1(A, rsel, ufast, dyn, (unsigned)wslots, s);
-            else if (G == 2 && ufast && A.fuse) regwide_launch_fused_g2(A, rsel, dyn, (unsigned)wslots, s);
             else if (G == 2) regwide_launch_g2(A, rsel, ufast, dyn, (unsigned)wslots, s);
             else if (G == 4) regwide_launch_g4(A, rsel, ufast, dyn, (unsigned)wslots, s);
             else regwide_launch_g8(A, rsel, ufast, dyn, (unsigned)wslots, s);
@@ -485,7 +425,6 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     Cw.gate = B.abortf;
     const int64_t ts = std::min<int64_t>(tailn, wslots > 1 ? wslots : slots);
     if (G == 1) regwide_launch_g1(Cw, rsel, ufast, dyn, (unsigned)ts, s);
-    else if (G == 2 && ufast && Cw.fuse) regwide_launch_fused_g2(Cw, rsel, dyn, (unsigned)ts, s);
     else if (G == 2) regwide_launch_g2(Cw, rsel, ufast, dyn, (unsigned)ts, s);
     else if (G == 4) regwide_launch_g4(Cw, rsel, ufast, dyn, (unsigned)ts, s);
     else regwide_launch_g8(Cw, rsel, ufast, dyn, (unsigned)ts, s);

@@ -97,8 +97,6 @@ struct RegArgs {
     const int32_t *gate;  // optional: solve the columns only if *gate != 0 (the whole-column
                           // re-solve of a split tail whose hand-offs gave up; read once at
                           // launch, wave-uniform), else every column as usual
-    int32_t fuse;         // launch the fused form (k_cg_regwide<..., FUSED>: the graph and
-                          // LDS layout passed k_fuse_check)
 };
 static constexpr int kRegPartTab = 4 * kRegMaxChunks + 4;
 
@@ -613,8 +611,6 @@ GS_REGWIDE_LAUNCH_DECL(2)
 GS_REGWIDE_LAUNCH_DECL(4)
 GS_REGWIDE_LAUNCH_DECL(8)
 #undef GS_REGWIDE_LAUNCH_DECL
-// fused p update, two threads per chain, unit weights (gs_cg_reg_g2.hip)
-void regwide_launch_fused_g2(const RegArgs &A, int R, size_t dyn, unsigned slots, hipStream_t s);
 // split form, 4 or 8 threads per chain (gs_cg_reg_s4.hip, gs_cg_reg_s8.hip)
 void regwide_split_launch_g4(const RegArgs &A, int R, bool unit, size_t dyn, unsigned grid, hipStream_t s);
 void regwide_split_launch_g8(const RegArgs &A, int R, bool unit, size_t dyn, unsigned grid, hipStream_t s);

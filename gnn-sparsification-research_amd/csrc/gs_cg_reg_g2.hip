@@ -6,5 +6,4 @@
 
 namespace gs {
 GS_REGWIDE_LAUNCH_DEF(2)
-GS_REGWIDE_FUSED_DEF(2)
 }  // namespace gs

@@ -57,7 +57,7 @@ __device__ __forceinline__ double wide_readlane(double v, int ln) {
 // drained-sc1 recipe: sc1 payload, s_waitcnt vmcnt(0), barrier, one sc1 flag store, sc1
 // polls.  The chunk dots are added in global chunk order, so the bits are those of
 // the one-workgroup solve.  Used for the last, partly occupied round of columns.
-template <int G, int R, bool UNIT, bool QR, bool SPLIT = false, bool FUSED = false>
+template <int G, int R, bool UNIT, bool QR, bool SPLIT = false>
 __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     constexpr int CW = 64 / G;  // chains per wave
     // V2 (whole columns, unit weights): each slot's "any p code global" and "any row
@@ -67,15 +67,6 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     // count's load, convert and add) -- the same bits as the count-derived value, which
     // is checked equal at setup for the unit form
     constexpr bool V2 = GS_CG_V2 && UNIT && !SPLIT;
-    // FUSE (V2, two threads per chain: wave w owns chunk w, slot u its rows 64 u ..
-    // 64 u + 63): the p update of slot u + 1 runs in the SpMV pass, right before slot u's
-    // gathers, instead of in a pass of its own behind a barrier -- slot 0, the slots past
-    // the LDS prefix and the tail rows (every row another wave may read) are updated
-    // before the barrier.  Needs every row's entries within its own chunk's slots <= its
-    // slot + 1 or among those rows (the host launches this form when k_fuse_check passed)
-    // (a compile-time form: a runtime switch between the two prologues costs ~250 VGPR
-    // spills in this kernel)
-    constexpr bool FUSE = FUSED && V2 && G == 2;
     extern __shared__ double lds[];
     const int part = SPLIT ? (int)(blockIdx.x % (unsigned)A.P) : 0;
     const int group = SPLIT ? (int)(blockIdx.x / (unsigned)A.P) : (int)blockIdx.x;
@@ -579,22 +570,12 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
 #pragma unroll
                 for (int u = 0; u < kPreP && u < R; ++u) pb4[u] = pload(u);
                 if constexpr (!SPLIT) {
-                    const uint32_t zaddr = (uint32_t)zslot * 8u, saddr = (uint32_t)(zslot + 1) * 8u;  // the scratch slot
-                    if constexpr (FUSE) {
-                        // slot 0 here; slots 1 .. ulds - 1 in the SpMV pass, the rest below
-                        if (0 < ulds) {
-                            const double po = lds_at(lds0());
-                            const double t1 = alpha_prev * po;
-                            x[0] = x[0] + t1;
-                            const double pb = po * beta;
-                            lds_put(valid(0) ? lds0() : saddr, pb + r[0]);
-                        }
-                    } else {
                     // two straight-line passes: every slot reads p_old from LDS (slots past
                     // the wave's LDS prefix read the zero slot and store to the scratch
                     // slot: x += alpha * 0 and p to scratch change nothing), then the slots
                     // past the prefix redo their update from the global p rows.  No branch
                     // between a prefetch and its use, so the waits count only what is needed.
+                    const uint32_t zaddr = (uint32_t)zslot * 8u, saddr = (uint32_t)(zslot + 1) * 8u;  // the scratch slot
                     double pf[R];
 #pragma unroll
                     for (int u = 0; u < kPreP && u < R; ++u) pf[u] = lds_at(u < ulds ? lds0() + 256u * G * u : zaddr);
@@ -611,7 +592,6 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                         const double pb = po * beta;
                         lds_put(u < ulds && valid(u) ? lds0() + 256u * G * u : saddr, pb + r[u]);
                         __builtin_amdgcn_sched_barrier(0);
-                    }
                     }
                     launder();
                     if constexpr (V2 && GS_PGRP > 0) {
@@ -721,25 +701,6 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                         eb[u + kPre] = ell_row(u + kPre);
                         if constexpr (V2) db[u + kPre] = diag_row(u + kPre);
                         else lb[u + kPre] = len_row(u + kPre);
-                    }
-                    if constexpr (FUSE) {
-                        if (u + 1 < R) {
-                            // fused p update of slot u + 1 (LDS prefix): its rows are read by
-                            // slot u's gathers (and later ones), all in this wave; a wave's
-                            // LDS operations complete in order
-                            if (u + 1 < ulds) {  // wave-uniform: the slot is in the LDS prefix
-                                // iteration 0 stores p = r (as SciPy's p = z.copy()) and leaves x
-                                const bool up = it > 0;  // wave-uniform
-                                const uint32_t pa = lds0() + 256u * G * (u + 1);
-                                const double po = lds_at(up ? pa : (uint32_t)zslot * 8u);
-                                const double t1 = alpha_prev * po;
-                                const double xn = x[u + 1] + t1;
-                                x[u + 1] = up ? xn : x[u + 1];
-                                const double pb = po * beta;
-                                const double pn = pb + r[u + 1];
-                                lds_put(valid(u + 1) ? pa : (uint32_t)(zslot + 1) * 8u, up ? pn : r[u + 1]);
-                            }
-                        }
                     }
                     double pv = 0.0, qv = 0.0;
                     if constexpr (V2) {
@@ -902,22 +863,6 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         };                                                                                    \
         (void)A.qreg; /* whole columns keep x in registers (the q-in-registers form of */     \
         pick(std::false_type{}); /* round 2 lives on only in the split tail) */               \
-    }
-
-// one launch of the fused form (two threads per chain, unit weights, x in registers):
-// the p update inside the SpMV pass (A.fuse: the graph passed k_fuse_check)
-#define GS_REGWIDE_FUSED_DEF(G_)                                                              \
-    void regwide_launch_fused_g##G_(const RegArgs &A, int R, size_t dyn, unsigned slots,     \
-                                    hipStream_t s) {                                          \
-        auto go = [&](auto kern) {                                                            \
-            GS_HIP(hipFuncSetAttribute((const void *)kern,                                    \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn)); \
-            kern<<<slots, kRegThreads, dyn, s>>>(A);                                          \
-        };                                                                                    \
-        if (R == 16) go(k_cg_regwide<G_, 16, true, false, false, true>);                      \
-        else if (R == 24) go(k_cg_regwide<G_, 24, true, false, false, true>);                 \
-        else if (R == 32) go(k_cg_regwide<G_, 32, true, false, false, true>);                 \
-        else go(k_cg_regwide<G_, 44, true, false, false, true>);                              \
     }
 
 // one launch of the split form (q in registers), grid = groups x A.P workgroups

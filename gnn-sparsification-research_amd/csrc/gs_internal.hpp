@@ -185,7 +185,6 @@ struct gs_ctx {
     // be resident: another process or stream held CUs)
     std::vector<int64_t> reg_ell_key, reg_split_key;
     int64_t reg_nov = 0;
-    int reg_fuse = 0;              // the ELL's graph and layout allow the fused p update
     std::vector<int64_t> reg_hch;  // host copy of the chunk table (outlives its async copy)
     bool reg_split_off = false;
     int64_t reg_split_off_epoch = -1;      // graph epoch the split form was turned off for
