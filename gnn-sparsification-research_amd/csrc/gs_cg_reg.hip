@@ -42,6 +42,10 @@ __device__ __forceinline__ int row_dslot(int32_t c, int T, const int64_t *__rest
     const int par = in ? ((o >> 5) / G) & 1 : 0;
     const int chain = t * 32 + j, CW = 64 / G;
     const int tid = (chain / CW) * 64 + (chain % CW) + CW * g;
+    if (dmul == 3) {  // k_cg_regwide's V2 two-per-chain layout (DPAD): bank of own p + 1
+        const int lb = (int)tab[3 * kRegMaxChunks + t];
+        return (tid & ~31) + ((lb + (tid & 31) + 1) & 31);
+    }
     return dmul == 2 ? 2 * tid + par : tid;
 }
 
@@ -133,7 +137,9 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     // sums / tail rows, the chunk table
     const int nch = 32 * T;
     const bool ufast = unit && dcount;  // the unit kernels derive every diagonal from the entry count
-    const int dsl = NT == 256 ? 2 * NT : ufast ? NT : 0;
+    // (512 threads, two per chain, unit: 32 more for the bank-aligned diagonal slots)
+    const bool dbank = NT == 512 && G == 2 && ufast;
+    const int dsl = NT == 256 ? 2 * NT : ufast ? NT + (dbank ? 32 : 0) : 0;
     const size_t lds_max = 160 * 1024;
     const int64_t cap =
         (int64_t)((lds_max - (6 * (size_t)nch + 2 * kRegMaxChunks + 2 + dsl) * 8) / 8);
@@ -208,9 +214,10 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     auto *ocol = (uint16_t *)c->buf("er_reg_ocol").ensure(sizeof(uint16_t) * (nov + 1));
     double *oval = ufast ? nullptr : (double *)c->buf("er_reg_oval").ensure(sizeof(double) * (nov + 1));
     if (fresh) {
-        k_ell8_fill<<<grid_for(n, 256, 8192), 256, 0, s>>>(0, (int32_t)n, T, dch, pad, G, NT == 256 ? 2 : 1,
-                                                          ufast ? (int32_t)zs + 2 : -1, lp, li, lv, optr,
-                                                          ell, ellv, ocol, oval, rflag);
+        k_ell8_fill<<<grid_for(n, 256, 8192), 256, 0, s>>>(0, (int32_t)n, T, dch, pad, G,
+                                                          NT == 256 ? 2 : dbank ? 3 : 1,
+                                                          ufast ? (dbank ? (int32_t)((zs + 2 + 31) & ~31) : (int32_t)zs + 2) : -1,
+                                                          lp, li, lv, optr, ell, ellv, ocol, oval, rflag);
         GS_HIP(hipGetLastError());
         c->reg_ell_key = key;
     }

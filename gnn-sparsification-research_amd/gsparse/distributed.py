@@ -257,8 +257,10 @@ def backbone_phases(nbatch: int, world: int, fractions=None) -> list[tuple[int, 
 
 
 # the ascending-count order's short searches decide most hub columns (reverse columns):
-# the ranks exchange their decisions at these fractions of the batch list
-BB_PHASES = (0.5, 0.8, 0.95)
+# the ranks exchange their decisions at these fractions of the batch list (RMAT-18, one
+# rank's stages run alone: 506 / 322 / 202 ms at N = 2 / 4 / 8 against 639 ms whole;
+# (0.5, 0.8, 0.95) 521 / 321 / 204, one range 840 / 509 / 303; tools/bb_stage_probe.py)
+BB_PHASES = (0.6, 0.9)
 
 
 def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
