@@ -33,7 +33,7 @@ __device__ __forceinline__ uint32_t p_code(int32_t c, int T, const int64_t *__re
 // chain row s of chain (t, j) is slot s / G of thread g = s % G; a chunk's tail rows
 // belong to g = 0 with parity 0
 __device__ __forceinline__ int row_dslot(int32_t c, int T, const int64_t *__restrict__ tab, int G,
-                                         int dmul) {
+                                         int dmul, int32_t d0 = 0) {
     int t = 0;
     while (t + 1 < T && c >= tab[t + 1]) ++t;
     const int o = (int)(c - tab[t]), n32 = (int)(tab[kRegMaxChunks + t] & ~(int64_t)31);
@@ -42,9 +42,10 @@ __device__ __forceinline__ int row_dslot(int32_t c, int T, const int64_t *__rest
     const int par = in ? ((o >> 5) / G) & 1 : 0;
     const int chain = t * 32 + j, CW = 64 / G;
     const int tid = (chain / CW) * 64 + (chain % CW) + CW * g;
-    if (dmul == 3) {  // k_cg_regwide's V2 two-per-chain layout (DPAD): bank of own p + 1
+    if (dmul == 3) {  // k_cg_regwide's V2 two-per-chain layout (DBANK): bank of own p + 1
         const int lb = (int)tab[3 * kRegMaxChunks + t];
-        return (tid & ~31) + ((lb + (tid & 31) + 1) & 31);
+        const int s0 = d0 + (tid & ~31);
+        return (tid & ~31) + ((lb + (tid & 31) + 1 - s0) & 31);
     }
     return dmul == 2 ? 2 * tid + par : tid;
 }
@@ -60,7 +61,7 @@ __global__ void k_ell8_fill(int32_t r0, int32_t n, int T, const int64_t *__restr
     for (int64_t i = r0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e0 = lp[i], len = lp[i + 1] - e0;
-        const uint32_t dcode = dslot0 >= 0 ? (uint32_t)(dslot0 + row_dslot((int32_t)i, T, tab, G, dmul)) : 0u;
+        const uint32_t dcode = dslot0 >= 0 ? (uint32_t)(dslot0 + row_dslot((int32_t)i, T, tab, G, dmul, dslot0)) : 0u;
         auto code = [&](int64_t e) -> uint32_t {
             return (dslot0 >= 0 && li[e] == i) ? dcode : p_code(li[e], T, tab);
         };
@@ -137,9 +138,9 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     // sums / tail rows, the chunk table
     const int nch = 32 * T;
     const bool ufast = unit && dcount;  // the unit kernels derive every diagonal from the entry count
-    // (512 threads, two per chain, unit: 32 more for the bank-aligned diagonal slots)
+    // (512 threads, two per chain, unit: the diagonal slots bank-permuted, k_cg_regwide DBANK)
     const bool dbank = NT == 512 && G == 2 && ufast;
-    const int dsl = NT == 256 ? 2 * NT : ufast ? NT + (dbank ? 32 : 0) : 0;
+    const int dsl = NT == 256 ? 2 * NT : ufast ? NT : 0;
     const size_t lds_max = 160 * 1024;
     const int64_t cap =
         (int64_t)((lds_max - (6 * (size_t)nch + 2 * kRegMaxChunks + 2 + dsl) * 8) / 8);
@@ -216,7 +217,7 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     if (fresh) {
         k_ell8_fill<<<grid_for(n, 256, 8192), 256, 0, s>>>(0, (int32_t)n, T, dch, pad, G,
                                                           NT == 256 ? 2 : dbank ? 3 : 1,
-                                                          ufast ? (dbank ? (int32_t)((zs + 2 + 31) & ~31) : (int32_t)zs + 2) : -1,
+                                                          ufast ? (int32_t)zs + 2 : -1,
                                                           lp, li, lv, optr, ell, ellv, ocol, oval, rflag);
         GS_HIP(hipGetLastError());
         c->reg_ell_key = key;

@@ -67,9 +67,9 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     // count's load, convert and add) -- the same bits as the count-derived value, which
     // is checked equal at setup for the unit form
     constexpr bool V2 = GS_CG_V2 && UNIT && !SPLIT;
-    // V2, two threads per chain: the diagonal slots start 32-aligned (32 doubles of room),
-    // each lane's slot in the bank after its own p rows' bank (see dslot below)
-    constexpr int DPAD = (V2 && G == 2) ? 32 : 0;
+    // V2, two threads per chain: each lane's diagonal slot in the bank after its own p
+    // rows' bank (see dslot below)
+    constexpr bool DBANK = V2 && G == 2;
     extern __shared__ double lds[];
     const int part = SPLIT ? (int)(blockIdx.x % (unsigned)A.P) : 0;
     const int group = SPLIT ? (int)(blockIdx.x / (unsigned)A.P) : (int)blockIdx.x;
@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     // slots, (unit form) one diagonal slot per thread, then chain sums, tail rows and
     // the chunk table
     double *sp = lds;
-    double *acc_pq = lds + zslot + 2 + (UNIT ? kRegThreads + DPAD : 0), *acc_rr = acc_pq + nch;
+    double *acc_pq = lds + zslot + 2 + (UNIT ? kRegThreads : 0), *acc_rr = acc_pq + nch;
     double *side_p = acc_pq + 2 * nch, *side_q = acc_pq + 3 * nch, *side_r = acc_pq + 4 * nch;
     double *side_x = acc_pq + 5 * nch;  // tail rows' r lives in side_r, x here
     // [4][kRegMaxChunks]: starts, lengths, LDS-resident prefix, its LDS base (SPLIT: then
@@ -241,13 +241,14 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     // the LDS (no fault; the value is replaced under one wave-uniform branch), so the
     // slot issues no memory load whose result it waits for -- the ELL rows prefetched
     // for the next slots stay in flight.
-    // (DPAD) lane l's slot sits in bank (own p bank + 1) mod 32 -- own rows lbase_t + l +
-    // 64 u -- so the diagonal reads of a gather collide less with the p reads of lanes
-    // whose entries are shifted by a lower chord (tools/lds_bank_sim.py: the gathers'
-    // extra LDS cycles on the Roman layout 40 % -> 35 % over conflict-free); k_ell8_fill
-    // (dmul 3) gives the diagonal entries the same codes
-    const int dslot = DPAD ? ((zslot + 2 + 31) & ~31) + (tid & ~31) + ((lbase_t + (tid & 31) + 1) & 31)
-                           : zslot + 2 + tid;
+    // (DBANK) each 32-lane group's slots stay the 32 after zslot + 2 + (tid & ~31), permuted
+    // so lane l's sits in bank (own p bank + 1) mod 32 -- own rows lbase_t + l + 64 u --
+    // and the diagonal reads of a gather collide less with the p reads of lanes whose
+    // entries are shifted by a lower chord (tools/lds_bank_sim.py: the gathers' extra LDS
+    // cycles on the Roman layout 40 % -> 35 % over conflict-free); k_ell8_fill (dmul 3)
+    // gives the diagonal entries the same codes
+    const int dslot0 = zslot + 2 + (tid & ~31);
+    const int dslot = DBANK ? dslot0 + ((lbase_t + (tid & 31) + 1 - dslot0) & 31) : zslot + 2 + tid;
     // u >= 0: register slot u (LDS fast path when u < ulds); u < 0: a tail row
     auto spmv = [&](int row, const uint4 e, int len, double &pown, int u) -> double {
         const bool fast = u >= 0 && u < ulds;  // wave-uniform
