@@ -53,10 +53,6 @@ static constexpr int kPreP = GS_KPRE_P;
 #define GS_CG_V2 1
 #endif
 // V2 p update: slots past the LDS prefix handled in groups of this many (one wait each)
-// V2 slots: the diagonal entry by a select instead of an LDS write before the gathers
-#ifndef GS_CG_DSEL
-#define GS_CG_DSEL 0
-#endif
 #ifndef GS_PGRP
 #define GS_PGRP 4
 #endif

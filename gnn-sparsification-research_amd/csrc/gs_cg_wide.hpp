@@ -313,23 +313,12 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         uint32_t ad[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) ad[k] = (k & 1) ? wide_code_addr<1>(w4[k >> 1]) : wide_code_addr<0>(w4[k >> 1]);
-#if GS_CG_DSEL
-        // the diagonal entry reads its (stale) slot with the other gathers and takes -td
-        // by a select afterwards: no write -> read round trip through LDS before the
-        // gathers, which issue at once with the own-row read
-        pown = fast ? lds_at(lds0() + 256u * G * u) : ldc(self);
-        double pv[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) pv[k] = lds_at(ad[k]);
-        const double td = dg * pown;
-#else
         pown = fast ? lds_at(lds0() + 256u * G * u) : ldc(self);
         const double td = dg * pown;
         spl[dslot] = -td;
         double pv[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) pv[k] = lds_at(ad[k]);
-#endif
         uint64_t gm = gmask;  // tested here, not hoisted (see launder)
         asm volatile("" : "+s"(gm));
         if ((gm >> u) & 1) {
@@ -343,27 +332,13 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             vm_drain();
         }
         double acc = 0.0;
-#if GS_CG_DSEL
-        const uint32_t dad = (uint32_t)dslot * 8u;
-        const double ntd = -td;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc = acc - (ad[k] == dad ? ntd : pv[k]);
-#else
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc = acc - pv[k];
-#endif
         uint64_t lm = lmask;
         asm volatile("" : "+s"(lm));
         if ((lm >> u) & 1) {  // rows longer than 8 entries: ocol
             const int64_t o0 = A.optr[row], o1 = A.optr[row + 1];
-#if GS_CG_DSEL
-            for (int64_t q = o0; q < o1; ++q) {
-                const int cc = (int)A.ocol[q];
-                acc = acc - (cc == dslot ? ntd : ldc(cc));
-            }
-#else
             for (int64_t q = o0; q < o1; ++q) acc = acc - ldc((int)A.ocol[q]);
-#endif
             vm_drain();
         }
         return acc;

@@ -556,6 +556,43 @@ def test_topk_large_with_ties_and_specials(gs):
     assert not m1.any()
 
 
+def test_topk_candidate_paths_vs_stable_argsort(gs, monkeypatch):
+    """The 12-bit first pass + candidate selection (default) and the 8-bit passes
+    (GSPARSE_TOPK=8) against np.argsort(kind='stable'): scores crowded into one
+    12-bit bucket (every candidate pass busy), NaNs, signed zeros, infinities."""
+    rng = np.random.default_rng(7)
+    nnz = 3 << 18
+    crowd = 1.0 + rng.integers(0, 4000, nnz) * 2.0 ** -40  # one 12-bit bucket, many ties
+    spread = rng.standard_normal(nnz)
+    spread[::1009] = np.nan
+    spread[::211] = -0.0
+    spread[::223] = 0.0
+    spread[7], spread[8] = np.inf, -np.inf
+    ctx = gs._lib.Context()
+    ctx.set_graph_csr(2, np.array([0, 1, 2]), np.array([1, 0], dtype=np.int32), None)
+    eng = gs.engine.Engine(ctx)
+    for s in (crowd, spread):
+        for mode in (None, "8"):
+            if mode:
+                monkeypatch.setenv("GSPARSE_TOPK", mode)
+            else:
+                monkeypatch.delenv("GSPARSE_TOPK", raising=False)
+            for frac in (0.01, 0.5, 0.97):
+                for low in (False, True):
+                    k = int(nnz * frac)
+                    mask, cut, nb, nt = eng.topk_mask(s, nnz + 3, k, low)
+                    idx = np.argsort(s, kind="stable")
+                    ref = np.zeros(nnz + 3, dtype=bool)
+                    ref[idx[:k] if low else idx[-k:]] = True
+                    assert np.array_equal(mask, ref), (mode, frac, low)
+                    sel = s[ref[:nnz]]
+                    c = np.nanmax(sel) if low else np.nanmin(sel)
+                    if not np.isnan(c):
+                        assert cut == c or (cut == 0 and c == 0)
+                        beyond = int((s < c).sum()) if low else int(((s > c) | np.isnan(s)).sum())
+                        assert nb == beyond and nt == int((s == c).sum()), (mode, frac, low)
+
+
 def test_edge_cases(gs):
     # isolated nodes, single edge, empty graph, self-loops + duplicates
     for ei, n in [(np.array([[0, 1], [1, 0]]), 5), (np.zeros((2, 0), dtype=np.int64), 3),
