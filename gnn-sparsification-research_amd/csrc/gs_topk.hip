@@ -161,13 +161,29 @@ __global__ void __launch_bounds__(256) k_pick12(Sel12 *st, int keep_lowest) {
     }
 }
 
+// one global atomic per wave and trip (the cut's bucket may hold millions of scores)
+__device__ __forceinline__ unsigned long long wave_slot(bool take, unsigned long long *cnt) {
+    const unsigned long long m = __ballot(take);
+    if (!m) return 0;
+    const int lane = threadIdx.x & 63;
+    const int leader = __builtin_ctzll(m);
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(cnt, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return base + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
+}
+
 __global__ void k_compact12(const double *__restrict__ s, int64_t nnz, Sel12 *__restrict__ st,
                             unsigned long long *__restrict__ cnt, uint64_t *__restrict__ ckey) {
     const uint64_t d = st->prefix >> 52;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nnz;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = order_key(s[i]);
-        if ((k >> 52) == d) ckey[atomicAdd(cnt, 1ull)] = k;
+    // every lane of a wave runs the same trips (the ballot needs the whole wave)
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t trips = (nnz + stride - 1) / stride;
+    for (int64_t tr = 0, i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; tr < trips; ++tr, i += stride) {
+        const uint64_t k = i < nnz ? order_key(s[i]) : 0ull;
+        const bool take = i < nnz && (k >> 52) == d;
+        const unsigned long long p = wave_slot(take, cnt);
+        if (take) ckey[p] = k;
     }
 }
 
@@ -229,11 +245,14 @@ __global__ void k_mask12(const double *__restrict__ s, int64_t nnz, const Sel12 
                          int keep_lowest, uint8_t *__restrict__ mask, unsigned long long *__restrict__ tcnt,
                          uint64_t *__restrict__ tidx) {
     const uint64_t t = st->prefix;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nnz;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = order_key(s[i]);
-        mask[i] = keep_lowest ? (k < t) : (k > t);
-        if (k == t) tidx[atomicAdd(tcnt, 1ull)] = (uint64_t)i;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t trips = (nnz + stride - 1) / stride;
+    for (int64_t tr = 0, i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; tr < trips; ++tr, i += stride) {
+        const uint64_t k = i < nnz ? order_key(s[i]) : 0ull;
+        if (i < nnz) mask[i] = keep_lowest ? (k < t) : (k > t);
+        const bool tie = i < nnz && k == t;
+        const unsigned long long p = wave_slot(tie, tcnt);
+        if (tie) tidx[p] = (uint64_t)i;
     }
 }
 
@@ -368,6 +387,11 @@ extern "C" int gs_topk_mask(gs_ctx *c, const double *scores, int s_loc, int64_t 
             GS_HIP(hipMemcpyAsync(hs + 1, &st->nbeyond_c, 16, hipMemcpyDeviceToHost, s));
             GS_HIP(hipMemcpyAsync(&key, &st->prefix, 8, hipMemcpyDeviceToHost, s));
             GS_HIP(hipStreamSynchronize(s));
+            if (getenv("GSPARSE_TOPK_DEBUG")) {
+                unsigned long long nc = 0;
+                GS_HIP(hipMemcpy(&nc, &st->ncand, 8, hipMemcpyDeviceToHost));
+                fprintf(stderr, "[topk] nnz=%lld candidates=%llu tied=%llu\n", (long long)nnz, nc, hs[2]);
+            }
             hbeyond = (int64_t)(hs[0] + hs[1]);
             htied = (int64_t)hs[2];
             hcut = key_to_double(key);

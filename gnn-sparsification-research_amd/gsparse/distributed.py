@@ -264,7 +264,8 @@ BB_PHASES = (0.6, 0.9)
 
 
 def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
-                     epsilon: float = 1e-9, stages=None, phases=None, keep_out=None):
+                     epsilon: float = 1e-9, stages=None, phases=None, keep_out=None,
+                     method: str | None = None):
     """metric_backbone keep mask over ranks (metric_backbone.py:86-111), staged
     (include/gsparse.h gs_bb_*): every rank searches the landmarks l = rank (mod N)
     (MIN all-reduce of the labels), certifies its column range and searches its
@@ -276,13 +277,32 @@ def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
     the comm device) and returns it.
 
     `stages`: a BackboneStages (default: one on the library's shared context), or a
-    stand-in with the same methods (the CPU tests)."""
+    stand-in with the same methods (the CPU tests).
+
+    `method`: "staged" (above) or "pairs" -- the round-4 split: both directions of a
+    pair decided by rank max(u, v) % N in one call (gs_metric_backbone_part), one SUM
+    all-reduce of the keep bytes.  Default: "pairs" at two ranks (RMAT-18, a rank's
+    work alone: 443 vs 506 ms staged), "staged" from three (N = 8: 202 vs 236 ms;
+    tools/bb_stage_probe.py, tools/bb_probe.py)."""
     from .metric_backbone import BackboneStages, check_weights
 
     E = (edge_index.shape[1] if not isinstance(edge_index, torch.Tensor)
          else int(edge_index.shape[1]))
     check_weights(edge_weights, E)
     st = stages if stages is not None else BackboneStages()
+    if method is None:
+        method = "pairs" if comm.world == 2 and hasattr(st, "pair_part") else "staged"
+    if method == "pairs":
+        keep = keep_out if keep_out is not None else torch.empty(max(E, 1), dtype=torch.uint8,
+                                                               device=comm.device)
+        st.pair_part(edge_index, num_nodes, edge_weights, epsilon, comm.rank, comm.world, keep)
+        if comm.world > 1 and E:
+            dist.all_reduce(keep[:E], op=dist.ReduceOp.SUM, group=comm.group)
+        if keep_out is not None:
+            return keep_out
+        return keep[:E].cpu().numpy().astype(bool)
+    if method != "staged":
+        raise ValueError(f"method must be 'staged' or 'pairs', got {method!r}")
     K = st.begin(edge_index, num_nodes, edge_weights, epsilon, comm.rank, comm.world)
     if K and comm.world > 1:
         D = torch.empty(K * num_nodes, dtype=torch.float64, device=comm.device)

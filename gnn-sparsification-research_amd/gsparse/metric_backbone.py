@@ -109,6 +109,31 @@ class BackboneStages:
         self.n, self.E, self.K = int(num_nodes), E, int(K.value)
         return self.K
 
+    def pair_part(self, edge_index, num_nodes: int, edge_weights, epsilon: float, part: int,
+                  nparts: int, keep):
+        """gs_metric_backbone_part: keep bytes of the columns (u, v) with max(u, v) %
+        nparts == part (ids as the library labels them), 0 elsewhere, into `keep`."""
+        if isinstance(edge_index, torch.Tensor) and edge_index.is_cuda:
+            src, dst = edge_index[0].contiguous(), edge_index[1].contiguous()
+            E = int(src.numel())
+        else:
+            ei = np.asarray(edge_index, dtype=np.int64)
+            E = ei.shape[1]
+            src, dst = np.ascontiguousarray(ei[0]), np.ascontiguousarray(ei[1])
+        if isinstance(edge_weights, torch.Tensor) and edge_weights.is_cuda:
+            w = edge_weights.reshape(-1)[:E].contiguous()
+        else:
+            w = np.ascontiguousarray(np.asarray(edge_weights, dtype=np.float64).reshape(-1)[:E])
+        check_weights(w, E)
+        (ps, loc), (pd, _), (pw, wloc), (pk, kloc) = self._p(src), self._p(dst), self._p(w), self._p(keep)
+        if loc != wloc:
+            raise ValueError("edge_index and edge_weights must be on the same side")
+        relax = ctypes.c_int64(0)
+        self.ctx.call("gs_metric_backbone_part", int(num_nodes), E, ps, pd, pw, len(w), loc,
+                      float(epsilon), int(part), int(nparts), pk, kloc, ctypes.byref(relax))
+        self.relax = relax.value
+        return keep
+
     def landmarks_io(self, D, complete, out: bool):
         (pD, loc), (pc, _) = self._p(D), self._p(complete)
         self.ctx.call("gs_bb_landmarks_io", pD, pc, loc, 0 if out else 1)

@@ -217,7 +217,9 @@ def _gloo_rank(rank, world, port, q):
         for name, (eb, nb_) in _bb_graphs().items():
             w = _bb_costs(eb, nb_)
             bbs[name] = sharded_backbone(comm, eb, nb_, w)
-            bbs[name + "-8phases"] = sharded_backbone(comm, eb, nb_, w, phases=[i / 8 for i in range(1, 8)])
+            bbs[name + "-8phases"] = sharded_backbone(comm, eb, nb_, w, phases=[i / 8 for i in range(1, 8)],
+                                                      method="staged")
+            bbs[name + "-pairs"] = sharded_backbone(comm, eb, nb_, w, method="pairs")
         if rank == 0:
             q.put((jac, er, masks, bbs))
     finally:
@@ -265,7 +267,7 @@ def test_ranks_sharing_the_gpu_over_gloo(gs, world, monkeypatch):
 
     for name, (eb, nb_) in _bb_graphs().items():
         ref = backbone_mask(eb, nb_, _bb_costs(eb, nb_))
-        for key in (name, name + "-8phases"):
+        for key in (name, name + "-8phases", name + "-pairs"):
             assert np.array_equal(bbs[key], ref), (key, int((bbs[key] != ref).sum()))
 
 
