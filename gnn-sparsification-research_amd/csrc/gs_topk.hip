@@ -173,33 +173,51 @@ __device__ __forceinline__ unsigned long long wave_slot(bool take, unsigned long
     return base + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-__global__ void k_compact12(const double *__restrict__ s, int64_t nnz, Sel12 *__restrict__ st,
-                            unsigned long long *__restrict__ cnt, uint64_t *__restrict__ ckey) {
+// block b compacts its range [b chunk, (b + 1) chunk) into the same range of ckey
+// (slots from an LDS counter, one LDS atomic per wave and trip): no global counter --
+// the cut's bucket may hold millions of scores (R-MAT-22: 7.7 M), and one global
+// atomic per wave on a single address took 12 ms
+__global__ void __launch_bounds__(256) k_compact12(const double *__restrict__ s, int64_t nnz, int64_t chunk,
+                                                   const Sel12 *__restrict__ st, uint64_t *__restrict__ ckey,
+                                                   unsigned int *__restrict__ bcount) {
+    __shared__ unsigned int n_loc;
+    if (threadIdx.x == 0) n_loc = 0;
+    __syncthreads();
     const uint64_t d = st->prefix >> 52;
-    // every lane of a wave runs the same trips (the ballot needs the whole wave)
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t trips = (nnz + stride - 1) / stride;
-    for (int64_t tr = 0, i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; tr < trips; ++tr, i += stride) {
-        const uint64_t k = i < nnz ? order_key(s[i]) : 0ull;
-        const bool take = i < nnz && (k >> 52) == d;
-        const unsigned long long p = wave_slot(take, cnt);
-        if (take) ckey[p] = k;
+    const int64_t b0 = (int64_t)blockIdx.x * chunk;
+    const int64_t b1 = b0 + chunk < nnz ? b0 + chunk : nnz;
+    const int lane = threadIdx.x & 63;
+    for (int64_t i0 = b0; i0 < b1; i0 += blockDim.x) {  // whole waves run every trip
+        const int64_t i = i0 + threadIdx.x;
+        const uint64_t k = i < b1 ? order_key(s[i]) : 0ull;
+        const bool take = i < b1 && (k >> 52) == d;
+        const unsigned long long m = __ballot(take);
+        if (m) {
+            const int leader = __builtin_ctzll(m);
+            unsigned int base = 0;
+            if (lane == leader) base = atomicAdd(&n_loc, (unsigned int)__popcll(m));
+            base = __shfl(base, leader, 64);
+            if (take) ckey[b0 + base + __popcll(m & ((1ull << lane) - 1ull))] = k;
+        }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) bcount[blockIdx.x] = n_loc;
 }
 
 // digit = bits [shift, shift + bits) of the candidates matching the prefix above it
-__global__ void __launch_bounds__(256) k_chist(const uint64_t *__restrict__ ckey, Sel12 *__restrict__ st,
-                                               int shift, int bits) {
+// (block b: the candidates of region b, bcount[b] of them from b chunk)
+__global__ void __launch_bounds__(256) k_chist(const uint64_t *__restrict__ ckey, const unsigned int *__restrict__ bcount,
+                                               int64_t chunk, Sel12 *__restrict__ st, int shift, int bits) {
     __shared__ unsigned int h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
     const uint64_t prefix = st->prefix;
     const uint64_t hmask = ~0ull << (shift + bits);
     const uint64_t dmask = (1ull << bits) - 1;
-    const int64_t nc = (int64_t)st->ncand;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nc;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = ckey[i];
+    const uint64_t *ck = ckey + (int64_t)blockIdx.x * chunk;
+    const int64_t nc = bcount[blockIdx.x];
+    for (int64_t i = threadIdx.x; i < nc; i += blockDim.x) {
+        const uint64_t k = ck[i];
         if ((k & hmask) == (prefix & hmask)) atomicAdd(&h[(k >> shift) & dmask], 1u);
     }
     __syncthreads();
@@ -219,14 +237,15 @@ __global__ void k_cpick(Sel12 *st, int shift) {
     for (int i = 0; i < 256; ++i) st->chist[i] = 0;
 }
 
-// beyond / tied among the candidates
-__global__ void k_ccount(const uint64_t *__restrict__ ckey, Sel12 *__restrict__ st, int keep_lowest) {
+// beyond / tied among the candidates (block b: region b)
+__global__ void __launch_bounds__(256) k_ccount(const uint64_t *__restrict__ ckey, const unsigned int *__restrict__ bcount,
+                                                int64_t chunk, Sel12 *__restrict__ st, int keep_lowest) {
     const uint64_t t = st->prefix;
-    const int64_t nc = (int64_t)st->ncand;
+    const uint64_t *ck = ckey + (int64_t)blockIdx.x * chunk;
+    const int64_t nc = bcount[blockIdx.x];
     unsigned long long b = 0, e = 0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nc;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = ckey[i];
+    for (int64_t i = threadIdx.x; i < nc; i += blockDim.x) {
+        const uint64_t k = ck[i];
         b += keep_lowest ? (k < t) : (k > t);
         e += k == t;
     }
@@ -368,15 +387,18 @@ extern "C" int gs_topk_mask(gs_ctx *c, const double *scores, int s_loc, int64_t 
             const unsigned g = grid_for(nnz, 256, 1024);
             k_hist12<<<g, 256, 0, s>>>(ds, nnz, st);
             k_pick12<<<1, 256, 0, s>>>(st, keep_lowest);
-            k_compact12<<<grid_for(nnz, 256, 2048), 256, 0, s>>>(ds, nnz, st, cnt, ckey);
-            const unsigned gc = grid_for(nnz / 16 + 1, 256, 512);
+            // regions: one per compaction workgroup
+            const int64_t nreg = std::max<int64_t>(1, std::min<int64_t>(2048, nnz / 8192 + 1));
+            const int64_t chunk = (nnz + nreg - 1) / nreg;
+            auto *bcount = (unsigned int *)c->buf("topk_bcount").ensure(sizeof(unsigned int) * nreg);
+            k_compact12<<<(unsigned)nreg, 256, 0, s>>>(ds, nnz, chunk, st, ckey, bcount);
             // the other 52 bits: six 8-bit digits (bits 51..4), then the last 4 bits
             for (int shift = 44; shift >= -4; shift -= 8) {
                 const int sh = shift < 0 ? 0 : shift, bits = shift < 0 ? 4 : 8;
-                k_chist<<<gc, 256, 0, s>>>(ckey, st, sh, bits);
+                k_chist<<<(unsigned)nreg, 256, 0, s>>>(ckey, bcount, chunk, st, sh, bits);
                 k_cpick<<<1, 1, 0, s>>>(st, sh);
             }
-            k_ccount<<<gc, 256, 0, s>>>(ckey, st, keep_lowest);
+            k_ccount<<<(unsigned)nreg, 256, 0, s>>>(ckey, bcount, chunk, st, keep_lowest);
             uint64_t *tidx = (uint64_t *)c->buf("topk_tidx").ensure(sizeof(uint64_t) * nnz);
             GS_HIP(hipMemsetAsync(cnt, 0, 8, s));
             k_mask12<<<grid_for(nnz, 256, 2048), 256, 0, s>>>(ds, nnz, st, keep_lowest, dm, cnt, tidx);
