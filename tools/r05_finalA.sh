@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-5 final A: the whole GPU suite, smoke(), the default bench line (CPU baseline
+# included), then the rocprofv3 summaries of the four workloads on these sources.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=${1:-gpurun_out/r05finalA}
+mkdir -p "$OUT"
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 900 --timeout-method thread \
+    -p no:cacheprovider > "$OUT/pytest.log" 2>&1
+rc=$?
+tail -1 "$OUT/pytest.log"
+[ $rc -eq 0 ] || { echo "pytest rc=$rc"; grep -E "^(FAILED|ERROR)" "$OUT/pytest.log" | head -20; exit 1; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1 || { echo "smoke rc=$?"; tail -20 "$OUT/smoke.log"; exit 1; }
+tail -1 "$OUT/smoke.log"
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > "$OUT/bench_roman.json" 2> "$OUT/bench_roman.err" || exit $?
+python3 -c "import json;a=json.load(open('$OUT/bench_roman.json'));print('roman ms/step',a['ms_per_step'],a['cpu_baseline']['value'])"
+for wl in roman rmat backbone arxiv; do
+  tools/profile_bench.sh "$OUT/prof_$wl" --workload $wl || { echo "profile $wl rc=$?"; exit 1; }
+  echo "$wl profiled"
+done
