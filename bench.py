@@ -84,9 +84,11 @@ def pmc_summary(workload: str):
     return None, None, stale or f"no PMC summary of workload {workload!r}"
 
 
-def kernel_counters(summ: dict, name: str):
+def kernel_counters(summ: dict, name: str, calls_per_step: float = 1.0):
     """Per-call counters of profiler entry `name`: the kernels of one call summed
-    (pipelines: the plan kernel or the whole-column launch runs once per call)."""
+    (pipelines: the plan kernel or the whole-column launch runs once per call).
+    `calls_per_step`: calls of the region per bench step in the live run (the
+    arxiv CG's batched kernels: one call per CG iteration)."""
     pre = PMC_KERNEL.get(name)
     if not summ or pre is None:
         return None
@@ -94,11 +96,13 @@ def kernel_counters(summ: dict, name: str):
             if k != "_meta" and (k.startswith("void " + pre) or k.startswith(pre))]
     if not hits:
         return None
-    calls = summ.get("_meta", {}).get("calls_per_run")
-    if calls:
-        # the profiled run made exactly `calls` calls of the region (tools/profile_bench.sh:
-        # one step, no box-order re-run): every kernel it launched, each weighted by its
-        # own launch count, divided by the calls -- the timed call's kernel mix
+    steps = summ.get("_meta", {}).get("calls_per_run")
+    if steps:
+        # the profiled run made exactly `steps` bench steps (tools/profile_bench.sh: one
+        # step, no box-order re-run), i.e. steps x calls_per_step calls of the region:
+        # every kernel it launched, each weighted by its own launch count, divided by the
+        # calls -- the timed call's kernel mix
+        calls = steps * max(1.0, calls_per_step)
         out = {}
         for _, v in hits:
             for c, x in v.items():
@@ -125,7 +129,7 @@ def kernel_counters(summ: dict, name: str):
 
 
 def make_roofline(name: str, avg_ms: float, bytes_per: float, launches: int, workload: str,
-                  world: int, flops_per: float | None = None) -> dict:
+                  world: int, flops_per: float | None = None, steps: int | None = None) -> dict:
     """Roofline of the dominant kernel.  Headline (`achieved`, `frac`): measured
     HBM-side traffic -- rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per call of the same
     sources (FETCH_SIZE counts half of a wide stream on gfx950, WRITE_SIZE is exact:
@@ -168,7 +172,7 @@ def make_roofline(name: str, avg_ms: float, bytes_per: float, launches: int, wor
         roof["basis"] = "no PMC at N > 1 (summaries are 1-GPU runs); see algorithmic"
         return fp64_headline(roof, {})
     summ, src, note = pmc_summary(workload)
-    ctr = kernel_counters(summ, name) if summ else None
+    ctr = kernel_counters(summ, name, launches / steps if steps else 1.0) if summ else None
     if ctr is None or "FETCH_SIZE_KB" not in ctr or "WRITE_SIZE_KB" not in ctr:
         roof["basis"] = f"no counters for {name}: {note or src}; see algorithmic"
         return fp64_headline(roof, {})
@@ -553,7 +557,7 @@ def bench_backbone(args, world, rank, local_rank, dev, dist):
         p = prof["metric_backbone"]
         key = f"backbone-{args.bb_graph}" + (str(args.bb_scale) if args.bb_graph == "rmat" else "")
         roofline = make_roofline("metric_backbone", p["ms"] / p["launches"], p["bytes"] / p["launches"],
-                                 p["launches"], key, world)
+                                 p["launches"], key, world, steps=args.steps)
         roofline["relaxations_per_launch_rank0"] = relax.value if comm is None else stages.relax
     result = {
         "metric": "scored edges/sec (metric backbone)", "value": round(E * args.steps / elapsed, 1),
@@ -939,7 +943,7 @@ def bench_scorers(args, world, rank, local_rank, dev, dist):
         prof, key=lambda kk: prof[kk]["ms"])
     p = prof[name]
     roofline = make_roofline(name, p["ms"] / p["launches"], p["bytes"] / p["launches"], p["launches"],
-                             "roman", world)
+                             "roman", world, steps=args.steps)
     result = {
         "metric": "scored edges/sec (Jaccard+AA+FeatCos+ApproxER)",
         "value": round(world * E * args.steps / elapsed, 1), "unit": "scored edges/s",
@@ -1207,7 +1211,7 @@ def main():
             lnnz = nnz - loops + n  # L_reg = diag(deg) - A + 1e-6 I: every diagonal stored
             flops = (2.0 * lnnz + 12.0 * n) * its
         roofline = make_roofline(name, p["ms"] / p["launches"], p["bytes"] / p["launches"],
-                                 p["launches"], args.workload, world, flops_per=flops)
+                                 p["launches"], args.workload, world, flops_per=flops, steps=args.steps)
     kernels = {k2: {"launches": v["launches"], "ms": round(v["ms"], 3)} for k2, v in prof.items()}
 
     result = {

@@ -3,10 +3,11 @@
 
 usage: pmc_summary.py [--calls=N] OUT.json DIR [DIR ...]
 
---calls=N: the profiled command made N calls of each profiled region (bench.py
---steps S --warmup W --box-order-steps 0: N = S + W); bench.py then divides
-every kernel's launches x per-launch counters of a region by N -- exactly the
-kernels one timed call launches, each weighted by its own launch count.
+--calls=N: the profiled command ran N bench steps (bench.py --steps S --warmup W
+--box-order-steps 0: N = S + W), recorded as _meta.calls_per_run; bench.py then
+divides every kernel's launches x per-launch counters of a region by N x the
+region's calls per step in its live run -- exactly the kernels one timed call
+launches, each weighted by its own launch count.
 
 The summary's "_meta" records the source hash of the libgsparse sources it
 profiled (tools/provenance.py) and the git HEAD; bench.py refuses to join
