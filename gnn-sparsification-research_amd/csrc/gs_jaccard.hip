@@ -402,6 +402,9 @@ struct JacBitProbe {
 // steps) -- the last two are 6-14 % faster per class run alone and 2-6 % slower
 // with the classes overlapping on their streams, which fill each other's idle
 // waves already.
+#ifndef GS_JAC_MASKLOAD
+#define GS_JAC_MASKLOAD 1
+#endif
 template <class Probe, int UL = kJacUnrollDef, int UP = UL>
 __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix, int64_t du,
                                                  int64_t lo, const JacStage &st,
@@ -418,10 +421,16 @@ __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
         constexpr int P = UP < U ? UP : U;
         int32_t xs[U];
 #pragma unroll
-        for (int t = 0; t < U; ++t) xs[t] = lp[t * 64];
-        if constexpr (MASK) {
-#pragma unroll
-            for (int t = 0; t < U; ++t) xs[t] = lane + t * 64 < left ? xs[t] : -1;
+        for (int t = 0; t < U; ++t) {
+            if constexpr (MASK && GS_JAC_MASKLOAD) {  // lanes past d_v issue no load (exec-masked)
+                xs[t] = -1;
+                if (lane + t * 64 < left) xs[t] = lp[t * 64];
+            } else if constexpr (MASK) {  // (round 5: every lane loads, then the mask)
+                const int32_t x = lp[t * 64];
+                xs[t] = lane + t * 64 < left ? x : -1;
+            } else {
+                xs[t] = lp[t * 64];
+            }
         }
 #pragma unroll
         for (int g = 0; g < U; g += P) {
