@@ -1133,6 +1133,166 @@ __global__ void __launch_bounds__(1024) k_bb_landmarks(
     }
 }
 
+// The same landmark searches spread over the whole GPU (large graphs): W workgroups per
+// landmark and one launch per frontier round -- the launch boundary is the round's
+// barrier and makes every label of the round visible to every CU of the next (a
+// single-workgroup search is one CU's throughput: 48 of them took 21.8 ms on RMAT-18,
+// and 6 per rank as long).  Labels are D's own words (IEEE bits; non-negative doubles
+// order as their bits), lowered by device-scope atomicMin; a label read for a check may
+// be older than this round's atomics, which costs a redundant atomic, never a missed
+// improvement (every improvement queues its node for the next round).  Frontier items
+// are (node, chunk of kLmChunk edges), so a hub's list is split over the waves of all W
+// workgroups; a node is queued for round r + 1 once (atomicMax of its round stamp).
+// The fixpoint -- the least one of d(y) = min_x fl(d(x) + w(x, y)) -- is the one the
+// one-workgroup search reaches; complete[l] = 0 when a landmark still had a frontier
+// after max_rounds rounds.
+static constexpr int kLmChunk = 256;
+// per landmark j (local index): counters cnt[4 j + (r mod 3)] = items of round r
+__global__ void k_lm_init(const int64_t *__restrict__ gp, const int32_t *__restrict__ lm, int K,
+                          int lpart, int lparts, int mine, int64_t cap,
+                          unsigned long long *__restrict__ D, uint64_t *__restrict__ items,
+                          int32_t *__restrict__ cnt) {
+    const int j = blockIdx.x;
+    if (j >= mine) return;
+    const int l = lpart + j * lparts;
+    const int32_t s = lm[l];
+    const int64_t d = gp[s + 1] - gp[s];
+    const int nch = (int)((d + kLmChunk - 1) / kLmChunk);
+    uint64_t *cur = items + (size_t)j * 2 * cap;
+    for (int c = threadIdx.x; c < nch; c += blockDim.x) cur[c] = (uint64_t)(uint32_t)s << 32 | (uint32_t)c;
+    if (threadIdx.x == 0) {
+        D[(int64_t)s * K + l] = 0ull;  // +0.0
+        cnt[4 * j] = nch;
+        cnt[4 * j + 1] = 0;
+        cnt[4 * j + 2] = 0;
+    }
+}
+
+template <int NT>
+__global__ void __launch_bounds__(NT) k_lm_round(
+    const int64_t *__restrict__ gp, const int32_t *__restrict__ gi, const double *__restrict__ gw,
+    int64_t n, int K, int lpart, int lparts, int W, int r, int64_t cap,
+    unsigned long long *__restrict__ D, uint64_t *__restrict__ items, uint32_t *__restrict__ stamp,
+    int32_t *__restrict__ cnt) {
+    constexpr int NW = NT / 64;
+    const int j = blockIdx.x / W, wb = blockIdx.x - j * W;
+    const int l = lpart + j * lparts;
+    int32_t *cj = cnt + 4 * j;
+    const int fc = cj[r % 3];
+    // the counter of round r + 2 was last read in round r - 1
+    if (wb == 0 && threadIdx.x == 0) cj[(r + 2) % 3] = 0;
+    if (fc == 0) return;  // workgroup-uniform
+    const uint64_t *cur = items + ((size_t)j * 2 + (r & 1)) * cap;
+    uint64_t *nxt = items + ((size_t)j * 2 + ((r + 1) & 1)) * cap;
+    uint32_t *st = stamp + (size_t)j * n;
+    int32_t *cn = cj + (r + 1) % 3;
+    const uint32_t rn = (uint32_t)r + 1u;
+    __shared__ int32_t w_pre[NW][65];
+    __shared__ int64_t w_beg[NW][64];
+    __shared__ double w_d[NW][64];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // items per wave: up to 64, fewer when the frontier is short (a hub's chunks in the
+    // first rounds would otherwise all fall to a few waves)
+    const int per = max(1, min(64, (fc + W * NW - 1) / (W * NW)));
+    for (int f0 = (wb * NW + wv) * per; f0 < fc; f0 += W * NW * per) {
+        const int f = f0 + lane;
+        int deg = 0;
+        int64_t b = 0;
+        double dx = 0.0;
+        if (lane < per && f < fc) {
+            const uint64_t it = cur[f];
+            const int32_t x = (int32_t)(it >> 32);
+            const int64_t a = gp[x] + (int64_t)(uint32_t)it * kLmChunk, e1 = gp[x + 1];
+            b = a;
+            deg = (int)(e1 - a < kLmChunk ? e1 - a : kLmChunk);
+            dx = __longlong_as_double((long long)D[(int64_t)x * K + l]);
+        }
+        int incl = deg;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += t;
+        }
+        const int total = __shfl(incl, 63, 64);
+        w_pre[wv][lane + 1] = incl;
+        if (lane == 0) w_pre[wv][0] = 0;
+        w_beg[wv][lane] = b;
+        w_d[wv][lane] = dx;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        constexpr int U = 4;  // edges per lane per trip, all loads in flight
+        for (int e0 = 0; e0 < total; e0 += 64 * U) {
+            int32_t y[U];
+            unsigned long long nb[U], cd[U];
+            bool go[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = e0 + u * 64 + lane;
+                go[u] = e < total;
+                const int ec = go[u] ? e : 0;
+                int lo = 0, hi = 63;  // largest k with w_pre[k] <= ec
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (w_pre[wv][mid] <= ec) lo = mid;
+                    else hi = mid - 1;
+                }
+                const int64_t ei = w_beg[wv][lo] + (ec - w_pre[wv][lo]);
+                nb[u] = (unsigned long long)__double_as_longlong(w_d[wv][lo] + gw[ei]);
+                y[u] = gi[ei];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) cd[u] = go[u] ? D[(int64_t)y[u] * K + l] : 0ull;
+            // the U atomics of a lane in flight together, then the stamps of the improved
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                go[u] = go[u] && nb[u] < cd[u];
+                cd[u] = go[u] ? atomicMin(&D[(int64_t)y[u] * K + l], nb[u]) : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) go[u] = go[u] && nb[u] < cd[u] && atomicMax(&st[y[u]], rn) < rn;
+            int nch[U], mine = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                nch[u] = go[u] ? (int)((gp[y[u] + 1] - gp[y[u]] + kLmChunk - 1) / kLmChunk) : 0;
+                mine += nch[u];
+            }
+            // one counter add per wave and trip (a single word takes ~90 adds per us)
+            int incl = mine;
+            for (int off = 1; off < 64; off <<= 1) {
+                const int t = __shfl_up(incl, off, 64);
+                if (lane >= off) incl += t;
+            }
+            const int wtot = __shfl(incl, 63, 64);
+            if (wtot) {
+                int base = 0;
+                if (lane == 63) base = atomicAdd(cn, wtot);
+                int q = __shfl(base, 63, 64) + incl - mine;
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    for (int c = 0; c < nch[u]; ++c) nxt[q++] = (uint64_t)(uint32_t)y[u] << 32 | (uint32_t)c;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+// sum of the next round's item counts of every landmark into *tot; complete flags
+// (final: the counts of round r)
+__global__ void k_lm_count(const int32_t *__restrict__ cnt, int mine, int r, int lpart, int lparts,
+                           unsigned long long *__restrict__ tot, int32_t *__restrict__ complete,
+                           int final) {
+    unsigned long long s = 0;
+    for (int j = threadIdx.x; j < mine; j += blockDim.x) {
+        const int c = cnt[4 * j + r % 3];
+        s += (unsigned long long)c;
+        if (final) complete[lpart + j * lparts] = c == 0;
+    }
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(tot, s);
+}
+
 // Full searches for sampled node pairs (verify_geodesic_preservation,
 // compute_geodesic_preservation): one workgroup per distinct source, then the
 // exact distance of each of its targets (+inf when unreachable).
@@ -1569,7 +1729,45 @@ static void bb_begin(gs_ctx *c, int64_t n, int64_t E, const int64_t *src, const 
             R.lcomp = (int32_t *)b_lcomp.ensure(4 * K);
             GS_HIP(hipMemsetAsync(R.lcomp, 0, 4 * K, s));
             const int mine = (K - lpart + lparts - 1) / lparts;  // landmarks l = lpart (mod lparts)
-            if (mine > 0) {
+            // large graphs: the searches spread over the GPU, one launch per round
+            // (k_lm_round; GSPARSE_BB_LMCOOP=0: one workgroup per landmark)
+            bool coop = n > 65536 && n < ((int64_t)1 << 31);
+            if (const char *e = getenv("GSPARSE_BB_LMCOOP")) coop = coop && atoi(e) != 0;
+            if (mine > 0 && coop) {
+                const int64_t cap = n + hgp[n] / kLmChunk + 64;  // items of one round, at most
+                uint64_t *items = (uint64_t *)c->buf("bb_lmitems").ensure(16 * (size_t)mine * cap);
+                uint32_t *stamp = (uint32_t *)b_qflag.ensure(4 * (size_t)mine * n);
+                int32_t *cnt = (int32_t *)c->buf("bb_lmcnt").ensure(16 * (size_t)mine);
+                unsigned long long *tot = R.misc + 6;
+                GS_HIP(hipMemsetAsync(stamp, 0, 4 * (size_t)mine * n, s));
+                k_lm_init<<<(unsigned)mine, 256, 0, s>>>(R.gp, dlm, K, lpart, lparts, mine, cap,
+                                                         (unsigned long long *)R.D, items, cnt);
+                // workgroups per landmark: about two 512-thread workgroups per CU in all
+                int W = (512 + mine - 1) / mine;
+                if (const char *e = getenv("GSPARSE_BB_LMW")) W = atoi(e);
+                W = std::max(1, std::min(W, 256));
+                int r = 0;
+                while (r < kBbLandmarkRounds) {
+                    k_lm_round<512><<<(unsigned)(mine * W), 512, 0, s>>>(
+                        R.gp, R.gi, R.gw, n, K, lpart, lparts, W, r, cap, (unsigned long long *)R.D,
+                        items, stamp, cnt);
+                    ++r;
+                    // every 8 rounds: stop once no landmark has a frontier
+                    if (r % 8 == 0 && r < kBbLandmarkRounds) {
+                        GS_HIP(hipMemsetAsync(tot, 0, 8, s));
+                        k_lm_count<<<1, 256, 0, s>>>(cnt, mine, r, lpart, lparts, tot, R.lcomp, 0);
+                        unsigned long long ht = 0;
+                        GS_HIP(hipMemcpyAsync(&ht, tot, 8, hipMemcpyDeviceToHost, s));
+                        GS_HIP(hipStreamSynchronize(s));
+                        if (ht == 0) break;
+                    }
+                }
+                GS_HIP(hipMemsetAsync(tot, 0, 8, s));
+                k_lm_count<<<1, 256, 0, s>>>(cnt, mine, r, lpart, lparts, tot, R.lcomp, 1);
+                GS_HIP(hipGetLastError());
+                if (getenv("GSPARSE_BB_DEBUG"))
+                    fprintf(stderr, "[backbone] landmarks %d of %d: %d rounds, %d workgroups each\n", mine, K, r, W);
+            } else if (mine > 0) {
                 unsigned long long *ldist = (unsigned long long *)b_dist.ensure(8 * (size_t)mine * n);
                 int32_t *lq = (int32_t *)b_qflag.ensure(4 * (size_t)mine * n);
                 int32_t *lfr = (int32_t *)b_fr.ensure(8 * (size_t)mine * n);

@@ -335,3 +335,40 @@ def test_staged_backbone_parts_vs_one_gpu(gs, nparts):
             for s in st:
                 keep, _ = s.finish()
                 assert np.array_equal(keep[:E].astype(bool), ref), (name, fractions)
+
+
+@pytest.mark.parametrize("nparts", [1, 3])
+def test_landmark_searches_spread_vs_one_workgroup(gs, nparts, monkeypatch):
+    """The landmark searches of gs_bb_begin spread over the GPU (k_lm_round: W
+    workgroups per landmark, one launch per round) reach the labels and completeness
+    flags of one workgroup per landmark bit for bit (R-MAT-17, Jaccard costs), for
+    every part's landmarks l = part (mod nparts)."""
+    from gsparse import graphs
+    from gsparse._lib import Context
+    from gsparse.metric_backbone import BackboneStages
+
+    dev = torch.device("cuda", 0)
+    ei, n = graphs.rmat(17, 8, seed=7), 1 << 17
+    w = _bb_costs(ei, n)
+    got = {}
+    for coop in ("1", "0"):
+        monkeypatch.setenv("GSPARSE_BB_LMCOOP", coop)
+        for W in (("3", "64") if coop == "1" else ("0",)):
+            monkeypatch.setenv("GSPARSE_BB_LMW", W)
+            for r in range(nparts):
+                st = BackboneStages(Context(0))
+                K = st.begin(ei, n, w, 1e-9, r, nparts)
+                assert K == 48
+                D = torch.empty(K * n, dtype=torch.float64, device=dev)
+                C = torch.empty(K, dtype=torch.int32, device=dev)
+                st.landmarks_io(D, C, out=True)
+                got[(coop, W, r)] = (D.cpu().numpy(), C.cpu().numpy())
+    for r in range(nparts):
+        D0, C0 = got[("0", "0", r)]
+        mine = np.arange(r, 48, nparts)
+        assert np.all(C0[mine] == 1)  # the one-workgroup searches ran dry
+        assert np.isfinite(D0.reshape(n, 48)[:, mine]).any()
+        for W in ("3", "64"):
+            D1, C1 = got[("1", W, r)]
+            assert np.array_equal(C1, C0), (W, r)
+            assert bits_equal(D1, D0), (W, r)
