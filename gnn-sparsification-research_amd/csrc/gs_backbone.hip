@@ -599,7 +599,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     int32_t *__restrict__ far_all, double delta, int cross, const uint64_t *__restrict__ skeys,
     const int64_t *__restrict__ sidx, const int64_t *__restrict__ rpos, int64_t E, double mrg,
     int rev, int64_t b0, int64_t b1, int part, int nparts,
-    unsigned long long *__restrict__ batch_next, unsigned long long *__restrict__ relax_total) {
+    unsigned long long *__restrict__ batch_next, unsigned long long *__restrict__ relax_total,
+    unsigned long long *__restrict__ trace) {
     static_assert(S >= 1 && S <= 16, "1..16 sources per workgroup");
     // queue bits of the per-node mask; the near-far order needs S more bits for the
     // far pile (S <= 8 only: 16 sources fill the word)
@@ -645,6 +646,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
         // rev: the batches from the last (the sources are in node order, i.e. by
         // descending column count after the relabeling)
         const int64_t bi = rev ? nbatch - 1 - bq : bq;
+        // GSPARSE_BB_TRACE: the batch's start / end on the constant clock and workgroup
+        const unsigned long long tb0 = trace ? (unsigned long long)wall_clock64() : 0ull;
         if (threadIdx.x < S) {
             const int64_t si = bi * S + threadIdx.x;
             s_src[threadIdx.x] = si < nsrc ? sources[si] : -1;
@@ -674,6 +677,17 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
         if (threadIdx.x < S)
             s_wmax[threadIdx.x] = s_wkey[threadIdx.x] ? dkey_val(s_wkey[threadIdx.x]) : -1.0;
         __syncthreads();
+        if (trace && threadIdx.x == 0) {  // the batch's largest bound and its column count
+            double bm = -1.0;
+            long long nc = 0;
+            for (int k = 0; k < S; ++k) {
+                bm = s_wmax[k] > bm ? s_wmax[k] : bm;
+                if (s_src[k] >= 0) nc += optr[s_src[k] + 1] - optr[s_src[k]];
+            }
+            trace[6 * bj + 3] = (unsigned long long)__double_as_longlong(bm);
+            trace[6 * bj + 4] = (unsigned long long)nc;
+        }
+        const unsigned long long relax0 = relax;
         // seed: every live source at its own node (sources are distinct nodes)
         if (threadIdx.x == 0) {
             int f = 0;
@@ -1066,6 +1080,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
             }
         }
         __syncthreads();
+        if (trace && relax != relax0) atomicAdd(&trace[6 * bj + 5], relax - relax0);
         const int tc = s_tcount;
         for (int t = threadIdx.x; t < tc; t += NT) {
             const int32_t y = touched[t];
@@ -1073,8 +1088,14 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
             for (int k = 0; k < S; ++k) dist[(int64_t)y * S + k] = kInfBits;
             qmask[y] = 0u;
         }
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
+            if (trace) {
+                trace[6 * bj] = tb0;
+                trace[6 * bj + 1] = (unsigned long long)wall_clock64();
+                trace[6 * bj + 2] = blockIdx.x;
+            }
             s_bq = batch_next ? (long long)atomicAdd(batch_next, 1ull) : (long long)(bj + gridDim.x);
+        }
         __syncthreads();
     }
     atomicAdd(&s_relax, relax);
@@ -1344,13 +1365,65 @@ __global__ void __launch_bounds__(256) k_bb_pairs(
 //  * landmark lower bound: d >= |D_l(u)-D_l(v)| - m (D_l(u)+D_l(v)), so
 //    w <= that proves w <= d <= fl(d + eps): keep; D_l(u) finite with D_l(v)
 //    infinite (or the reverse) means u and v are disconnected: d = inf, keep.
+//  * local bounds (mw != null): every u-v path but the edge itself starts with
+//    another edge of u and ends with another edge of v, so its fold is at least
+//    LB = fl(mu' + mv') (1 - 2m), mu' / mv' the least weights of u's / v's other
+//    G edges (+inf: none).  With the edge in G (weight w_G, d <= w_G):
+//    w > fl(w_G + eps) proves w > fl(d + eps): prune; else w <= LB proves
+//    w <= fl(d + eps) whichever path is shortest: keep.  Without it every path is
+//    another one: w <= LB keeps.  (A column whose endpoint's edges all cost far more
+//    than the column -- the Jaccard-0 edges of R-MAT -- is kept here instead of by a
+//    search exhausting the giant component.)
 // m = max(1e-8, 8 n 2^-53) bounds the relative rounding of folds over simple
 // paths (< n terms each, two of them per walk).
+// per node of G: its least edge weight mw[2x] and the second least mw[2x + 1] (equal
+// when tied, +inf when missing), ma[x] the neighbour of the least; one wave per node
+__global__ void k_bb_minw(const int64_t *__restrict__ gp, const int32_t *__restrict__ gi,
+                          const double *__restrict__ gw, int64_t n, double *__restrict__ mw,
+                          int32_t *__restrict__ ma) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const double inf = __builtin_inf();
+    for (int64_t x = w0; x < n; x += nw) {
+        double m1 = inf, m2 = inf;
+        int32_t a1 = 0x7fffffff;
+        for (int64_t e = gp[x] + lane; e < gp[x + 1]; e += 64) {
+            const double we = gw[e];
+            const int32_t y = gi[e];
+            if (we < m1 || (we == m1 && y < a1)) {
+                m2 = m1;
+                m1 = we;
+                a1 = y;
+            } else if (we < m2) {
+                m2 = we;
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) {  // merge the lanes' (least, neighbour, second)
+            const double o1 = __shfl_xor(m1, off, 64), o2 = __shfl_xor(m2, off, 64);
+            const int32_t oa = __shfl_xor(a1, off, 64);
+            if (o1 < m1 || (o1 == m1 && oa < a1)) {
+                m2 = m1 < o2 ? m1 : o2;
+                m1 = o1;
+                a1 = oa;
+            } else {
+                m2 = o1 < m2 ? o1 : m2;
+            }
+        }
+        if (lane == 0) {
+            mw[2 * x] = m1;
+            mw[2 * x + 1] = m2;
+            ma[x] = a1;
+        }
+    }
+}
+
 __global__ void k_bb_certify(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
                              const double *__restrict__ w, int64_t c0, int64_t c1,
                              const int64_t *__restrict__ gp, const int32_t *__restrict__ gi,
                              const double *__restrict__ gw, const double *__restrict__ D,
                              const int32_t *__restrict__ complete, int K, double eps, double m,
+                             const double *__restrict__ mw, const int32_t *__restrict__ ma,
                              uint8_t *__restrict__ state) {
     for (int64_t i = c0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < c1;
          i += (int64_t)gridDim.x * blockDim.x) {
@@ -1362,6 +1435,30 @@ __global__ void k_bb_certify(const int64_t *__restrict__ src, const int64_t *__r
             const double wg = du == 1 && gi[gp[u]] == v ? gw[gp[u]] : gw[gp[v]];
             state[i] = (wi <= wg + eps) ? 1 : 2;  // d = fl(0 + w_G) = w_G
             continue;
+        }
+        if (mw && u != v) {
+            // w_G(u, v): v in the shorter of the two (sorted, symmetric) lists
+            const bool us = du <= dv;
+            int64_t lo = us ? gp[u] : gp[v], hi = us ? gp[u + 1] : gp[v + 1];
+            const int32_t key = (int32_t)(us ? v : u);
+            const int64_t end = hi;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (gi[mid] < key) lo = mid + 1;
+                else hi = mid;
+            }
+            const bool has = lo < end && gi[lo] == key;
+            const double mu = ma[u] == (int32_t)v ? mw[2 * u + 1] : mw[2 * u];
+            const double mv = ma[v] == (int32_t)u ? mw[2 * v + 1] : mw[2 * v];
+            const double lb = (mu + mv) * (1.0 - 2.0 * m);  // +inf when either is missing
+            if (has && wi > gw[lo] + eps) {
+                state[i] = 2;
+                continue;
+            }
+            if (wi <= lb) {
+                state[i] = 1;
+                continue;
+            }
         }
         uint8_t st = 0;
         for (int l = 0; l < K && !st; ++l) {
@@ -1801,11 +1898,21 @@ static void bb_certify(gs_ctx *c, int part, int nparts) {
     if (c1 > c0) {
         k_bb_witness<<<grid_for(c1 - c0, 256, 8192), 256, 0, s>>>(
             R.dsrc, R.ddst, R.dw, c0, c1, R.gp, R.gi, R.gw, R.eps, R.pair_part, R.pair_nparts, R.state);
-        if (R.K > 0) {
+        // local bounds (k_bb_certify; GSPARSE_BB_LOCALLB=0: off)
+        bool local = true;
+        if (const char *e = getenv("GSPARSE_BB_LOCALLB")) local = atoi(e) != 0;
+        double *mw = nullptr;
+        int32_t *ma = nullptr;
+        if (local && R.n > 0) {
+            mw = (double *)c->buf("bb_minw").ensure(16 * (size_t)R.n);
+            ma = (int32_t *)c->buf("bb_mina").ensure(4 * (size_t)R.n);
+            k_bb_minw<<<grid_for(R.n * 64, 256, 16384), 256, 0, s>>>(R.gp, R.gi, R.gw, R.n, mw, ma);
+        }
+        if (R.K > 0 || local) {
             const double mrg = std::max(1e-8, 8.0 * (double)R.n * 0x1p-53);
             k_bb_certify<<<grid_for(c1 - c0, 256, 8192), 256, 0, s>>>(R.dsrc, R.ddst, R.dw, c0, c1, R.gp,
                                                                        R.gi, R.gw, R.D, R.lcomp, R.K,
-                                                                       R.eps, mrg, R.state);
+                                                                       R.eps, mrg, mw, ma, R.state);
         }
         GS_HIP(hipGetLastError());
     }
@@ -1947,12 +2054,21 @@ static void bb_search(gs_ctx *c, int64_t b0, int64_t b1, int part, int nparts) {
         if (bnext) GS_HIP(hipMemsetAsync(bnext, 0, 8, s));
         const double mrg = std::max(1e-8, 8.0 * (double)R.n * 0x1p-53);
         auto *qm = (uint32_t *)R.qflag;
+        // GSPARSE_BB_TRACE=file: each batch's start / end (constant clock, 100 MHz) and
+        // workgroup, one JSON line per launch appended to the file (waits for the launch)
+        const char *tpath = getenv("GSPARSE_BB_TRACE");
+        unsigned long long *trace = nullptr;
+        if (tpath) {
+            trace = (unsigned long long *)c->buf("bb_trace").ensure(48 * (size_t)mine);
+            GS_HIP(hipMemsetAsync(trace, 0, 48 * (size_t)mine, s));
+        }
 #define GS_BBM(NT_, S_)                                                                          \
     k_bb_sssp_multi<NT_, S_><<<grid, NT_, 0, s>>>(R.gp, R.gi, R.gw, R.n, R.sources, R.nsrc, R.optr, \
                                                    R.order, R.ddst, R.dw, R.eps, R.state, R.dist,  \
                                                    qm, R.fr, R.fm, R.touched, R.farl, R.delta,     \
                                                    R.cross, R.skeys, R.sidx, R.rpos, R.E, mrg,     \
-                                                   R.rev, b0, b1, part, nparts, bnext, R.misc + 1)
+                                                   R.rev, b0, b1, part, nparts, bnext, R.misc + 1, \
+                                                   trace)
         const int S = R.S;
         if (R.bt == 1024) {
             if (S == 2) GS_BBM(1024, 2); else if (S == 4) GS_BBM(1024, 4);
@@ -1965,6 +2081,23 @@ static void bb_search(gs_ctx *c, int64_t b0, int64_t b1, int part, int nparts) {
             else if (S == 8) GS_BBM(256, 8); else GS_BBM(256, 16);
         }
 #undef GS_BBM
+        if (tpath) {
+            std::vector<unsigned long long> h(6 * (size_t)mine);
+            GS_HIP(hipMemcpyAsync(h.data(), trace, 48 * (size_t)mine, hipMemcpyDeviceToHost, s));
+            GS_HIP(hipStreamSynchronize(s));
+            if (FILE *f = fopen(tpath, "a")) {
+                fprintf(f, "{\"part\": %d, \"nparts\": %d, \"b0\": %lld, \"b1\": %lld, \"S\": %d, \"grid\": %u, \"rec\": [",
+                        part, nparts, (long long)b0, (long long)b1, R.S, grid);
+                for (int64_t i = 0; i < mine; ++i) {
+                    double bm;
+                    memcpy(&bm, &h[6 * i + 3], 8);
+                    fprintf(f, "%s[%llu, %llu, %llu, %.9g, %llu, %llu]", i ? ", " : "", h[6 * i], h[6 * i + 1],
+                            h[6 * i + 2], bm, h[6 * i + 4], h[6 * i + 5]);
+                }
+                fprintf(f, "]}\n");
+                fclose(f);
+            }
+        }
     }
     GS_HIP(hipGetLastError());
     prof_end(c, tp, "bb_search", 0.0);
