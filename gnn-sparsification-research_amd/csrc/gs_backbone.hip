@@ -1958,19 +1958,19 @@ static void bb_plan(gs_ctx *c) {
             // plain search preferred 256 x 1,024); small ones (many short searches):
             // 1,024 workgroups of 256 (Roman: 2.2 vs 3.0 ms)
             const bool big = n > 65536;
-            // a rank of 4 or more (staged form) has few batches per workgroup and waits on
+            // a rank of 8 or more (staged form) has few batches per workgroup and waits on
             // single searches: 2 sources per workgroup of 1,024 threads, 256 workgroups
-            // (RMAT-18 at N = 8: 202 ms per rank vs 258 ms with one GPU's geometry, which
-            // takes 738 vs 639 ms whole; tools/bb_stage_probe.py, profiles/r05d_*)
-            const bool wide = big && R.nranks >= 4;
+            // (RMAT-18 at N = 8: 120.5 ms per rank vs 131.5 ms with 8 sources x 512
+            // threads; at N = 4 the latter wins, 188.8 vs 204.9 ms; tools/bb_stage_probe.py,
+            // profiles/r05t_*)
+            const bool wide = big && R.nranks >= 8;
             int64_t maxslabs = big ? (wide ? 256 : 512) : 1024;
             if (const char *e = getenv("GSPARSE_BB_SLABS")) maxslabs = atoi(e) > 0 ? atoi(e) : maxslabs;
-            // sources searched together per workgroup (k_bb_sssp_multi), 1 = alone: 8 on
-            // large graphs, with the near-far order (RMAT-18: 692 ms; 16 sources, which
-            // leave no mask bits for the far pile, 725 ms -- before the reverse-column
-            // decisions 16 led, 1.85 vs 2.15 s), alone on small ones (Roman: 2.30 ms vs
-            // 2.45 ms with 8)
-            int S = big ? (wide ? 2 : 8) : 1;
+            // sources searched together per workgroup (k_bb_sssp_multi), 1 = alone: on
+            // large graphs 16 on one GPU (RMAT-18 with the local-bound certificates: 455.9
+            // vs 475.8 ms with 8, which keep the near-far order), 8 per rank of 2 to 7 (N = 4:
+            // 188.8 ms; 16: 219.7); alone on small ones (Roman: 2.30 ms vs 2.45 ms with 8)
+            int S = big ? (wide ? 2 : R.nranks == 1 ? 16 : 8) : 1;
             if (const char *e = getenv("GSPARSE_BB_MULTI")) {
                 const int v = atoi(e);
                 S = v >= 16 ? 16 : v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;

@@ -250,7 +250,8 @@ def backbone_phases(nbatch: int, world: int, fractions=None) -> list[tuple[int, 
         return [(0, nbatch)]
     if fractions is None:
         env = os.environ.get("GSPARSE_BB_PHASES")
-        fractions = [float(x) for x in env.split(",") if x.strip()] if env else BB_PHASES
+        fractions = ([float(x) for x in env.split(",") if x.strip()] if env
+                     else BB_PHASES_4 if 4 <= world < 8 else BB_PHASES)
     cuts = sorted({int(round(f * nbatch)) for f in fractions if 0.0 < f < 1.0})
     bounds = [0] + [c for c in cuts if 0 < c < nbatch] + [nbatch]
     return list(zip(bounds[:-1], bounds[1:]))
@@ -258,9 +259,11 @@ def backbone_phases(nbatch: int, world: int, fractions=None) -> list[tuple[int, 
 
 # the ascending-count order's short searches decide most hub columns (reverse columns):
 # the ranks exchange their decisions at these fractions of the batch list (RMAT-18, one
-# rank's stages run alone: 506 / 322 / 202 ms at N = 2 / 4 / 8 against 639 ms whole;
-# (0.5, 0.8, 0.95) 521 / 321 / 204, one range 840 / 509 / 303; tools/bb_stage_probe.py)
-BB_PHASES = (0.6, 0.9)
+# rank's stages run alone, with the local-bound certificates: (0.7, 0.9) 276.6 / 173.8 /
+# 116.7 ms at N = 2 / 4 / 8 against 454.9 ms whole; (0.6, 0.9) 286.5 / 187.8 / 122.1;
+# (0.8) 281.7 / 163.8 / 118.9; tools/bb_stage_probe.py, profiles/r05u_*)
+BB_PHASES = (0.7, 0.9)
+BB_PHASES_4 = (0.8,)  # 4 to 7 ranks
 
 
 def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
@@ -281,9 +284,9 @@ def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
 
     `method`: "staged" (above) or "pairs" -- the round-4 split: both directions of a
     pair decided by rank max(u, v) % N in one call (gs_metric_backbone_part), one SUM
-    all-reduce of the keep bytes.  Default: "pairs" at two ranks (RMAT-18, a rank's
-    work alone: 443 vs 506 ms staged), "staged" from three (N = 8: 202 vs 236 ms;
-    tools/bb_stage_probe.py, tools/bb_probe.py)."""
+    all-reduce of the keep bytes.  Default: "staged" (RMAT-18, a rank's work alone:
+    276.6 vs 315.9 ms at N = 2, 116.7 vs 185.4 ms at N = 8; tools/bb_stage_probe.py,
+    tools/bb_probe.py, profiles/r05u_*)."""
     from .metric_backbone import BackboneStages, check_weights
 
     E = (edge_index.shape[1] if not isinstance(edge_index, torch.Tensor)
@@ -291,7 +294,7 @@ def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
     check_weights(edge_weights, E)
     st = stages if stages is not None else BackboneStages()
     if method is None:
-        method = "pairs" if comm.world == 2 and hasattr(st, "pair_part") else "staged"
+        method = "staged"
     if method == "pairs":
         keep = keep_out if keep_out is not None else torch.empty(max(E, 1), dtype=torch.uint8,
                                                                device=comm.device)
