@@ -150,6 +150,7 @@ __global__ void k_bb_witness(const int64_t *__restrict__ src, const int64_t *__r
             state[i] = 3;  // another part's column: not decided here
             continue;
         }
+        if (state[i] != 0) continue;  // decided by k_bb_certify (it runs first)
         double wi = w[i];
         if (u == v) {  // d(u,u) = 0
             state[i] = (wi <= 0.0 + eps) ? 1 : 2;
@@ -1424,11 +1425,13 @@ __global__ void k_bb_certify(const int64_t *__restrict__ src, const int64_t *__r
                              const double *__restrict__ gw, const double *__restrict__ D,
                              const int32_t *__restrict__ complete, int K, double eps, double m,
                              const double *__restrict__ mw, const int32_t *__restrict__ ma,
-                             uint8_t *__restrict__ state) {
+                             int part, int nparts, uint8_t *__restrict__ state) {
     for (int64_t i = c0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < c1;
          i += (int64_t)gridDim.x * blockDim.x) {
         if (state[i] != 0) continue;  // decided, or another part's column (3)
         const int64_t u = src[i], v = dst[i];
+        // another part's column (pair form) and self-loops: k_bb_witness's
+        if (u == v || (nparts > 1 && bb_col_part(u, v, nparts) != part)) continue;
         const double wi = w[i];
         const int64_t du = gp[u + 1] - gp[u], dv = gp[v + 1] - gp[v];
         if ((du == 1 && gi[gp[u]] == v) || (dv == 1 && gi[gp[v]] == u)) {
@@ -1436,7 +1439,7 @@ __global__ void k_bb_certify(const int64_t *__restrict__ src, const int64_t *__r
             state[i] = (wi <= wg + eps) ? 1 : 2;  // d = fl(0 + w_G) = w_G
             continue;
         }
-        if (mw && u != v) {
+        if (mw) {
             // w_G(u, v): v in the shorter of the two (sorted, symmetric) lists
             const bool us = du <= dv;
             int64_t lo = us ? gp[u] : gp[v], hi = us ? gp[u + 1] : gp[v + 1];
@@ -1896,8 +1899,9 @@ static void bb_certify(gs_ctx *c, int part, int nparts) {
     const int64_t E = R.E, c0 = E * part / nparts, c1 = E * (part + 1) / nparts;
     hipEvent_t tp = prof_begin(c);
     if (c1 > c0) {
-        k_bb_witness<<<grid_for(c1 - c0, 256, 8192), 256, 0, s>>>(
-            R.dsrc, R.ddst, R.dw, c0, c1, R.gp, R.gi, R.gw, R.eps, R.pair_part, R.pair_nparts, R.state);
+        // the certificates first (landmarks, local bounds: O(K) / O(log d) per column), then
+        // the 2-hop witnesses of the columns still open -- a merge of both endpoints'
+        // lists, which the hub-hub columns the landmark labels decide made the dearest
         // local bounds (k_bb_certify; GSPARSE_BB_LOCALLB=0: off)
         bool local = true;
         if (const char *e = getenv("GSPARSE_BB_LOCALLB")) local = atoi(e) != 0;
@@ -1912,8 +1916,11 @@ static void bb_certify(gs_ctx *c, int part, int nparts) {
             const double mrg = std::max(1e-8, 8.0 * (double)R.n * 0x1p-53);
             k_bb_certify<<<grid_for(c1 - c0, 256, 8192), 256, 0, s>>>(R.dsrc, R.ddst, R.dw, c0, c1, R.gp,
                                                                        R.gi, R.gw, R.D, R.lcomp, R.K,
-                                                                       R.eps, mrg, mw, ma, R.state);
+                                                                       R.eps, mrg, mw, ma, R.pair_part,
+                                                                       R.pair_nparts, R.state);
         }
+        k_bb_witness<<<grid_for(c1 - c0, 256, 8192), 256, 0, s>>>(
+            R.dsrc, R.ddst, R.dw, c0, c1, R.gp, R.gi, R.gw, R.eps, R.pair_part, R.pair_nparts, R.state);
         GS_HIP(hipGetLastError());
     }
     prof_end(c, tp, "bb_certify", 0.0);
@@ -1929,9 +1936,11 @@ static void bb_plan(gs_ctx *c) {
     hipStream_t s = c->stream;
     const int64_t n = R.n, E = R.E;
     R.nsrc = R.nbatch = 0;
+    hipEvent_t tp = prof_begin(c);
     if (E > 0) {
         int64_t *flag = (int64_t *)c->buf("bb_flag").ensure(8 * (n + 1));
         int64_t *pos = (int64_t *)c->buf("bb_pos").ensure(8 * (n + 1));
+        hipEvent_t tq = prof_begin(c);
         k_bb_need<<<grid_for(n, 256, 8192), 256, 0, s>>>(R.optr, R.order, R.state, n, flag);
         exclusive_scan_i64(c, flag, pos, n);
         int64_t lastp = 0, lastf = 0;
@@ -1940,6 +1949,7 @@ static void bb_plan(gs_ctx *c) {
             GS_HIP(hipMemcpyAsync(&lastf, flag + n - 1, 8, hipMemcpyDeviceToHost, s));
         }
         GS_HIP(hipStreamSynchronize(s));
+        prof_end(c, tq, "bb_plan_need", 0.0);
         R.nsrc = lastp + lastf;
         if (getenv("GSPARSE_BB_DEBUG")) {
             GS_HIP(hipMemsetAsync(R.misc + 3, 0, 8, s));
@@ -1984,6 +1994,7 @@ static void bb_plan(gs_ctx *c) {
             if (cap < 1) cap = 1;
             if (slabs > cap) slabs = cap;
             R.slabs = slabs;
+            hipEvent_t tf = prof_begin(c);
             R.dist = (unsigned long long *)c->buf("bb_dist").ensure(8 * (size_t)S * slabs * n);
             R.qflag = (int32_t *)c->buf("bb_qflag").ensure(4 * slabs * n);
             R.fr = (int32_t *)c->buf("bb_fr").ensure(8 * slabs * n);
@@ -1991,6 +2002,7 @@ static void bb_plan(gs_ctx *c) {
             k_bb_fill_u64<<<grid_for((int64_t)S * slabs * n, 256, 65536), 256, 0, s>>>(
                 R.dist, (int64_t)S * slabs * n, kInfBits);
             GS_HIP(hipMemsetAsync(R.qflag, 0, 4 * slabs * n, s));
+            prof_end(c, tf, "bb_plan_fill", 0.0);
             R.bt = big ? (wide ? 1024 : 512) : 256;
             if (const char *e = getenv("GSPARSE_BB_THREADS")) R.bt = atoi(e) == 1024 ? 1024 : atoi(e) == 512 ? 512 : 256;
             if (S > 1) {
@@ -2000,6 +2012,7 @@ static void bb_plan(gs_ctx *c) {
                 if (const char *e = getenv("GSPARSE_BB_CROSS")) R.cross = atoi(e) != 0;
                 R.skeys = nullptr;
                 R.sidx = R.rpos = nullptr;
+                hipEvent_t tc = prof_begin(c);
                 if (R.cross) {
                     R.skeys = (uint64_t *)c->buf("bb_skeys").ensure(8 * E);
                     R.sidx = (int64_t *)c->buf("bb_sidx").ensure(8 * E);
@@ -2008,6 +2021,7 @@ static void bb_plan(gs_ctx *c) {
                     sort_pairs_u64_i64(c, R.skeys, R.sidx, E, bits_for_bb((uint64_t)n * (uint64_t)n));
                     k_bb_revpos<<<grid_for(E, 256, 8192), 256, 0, s>>>(R.dsrc, R.ddst, E, n, R.skeys, R.rpos);
                 }
+                prof_end(c, tc, "bb_plan_cross", 0.0);
                 // sources by ascending column count (the batches from the last): the
                 // short searches first, so their reverse-column decisions close most of
                 // the hubs' targets before the hubs search (RMAT-18 1.63 -> 0.83 s;
@@ -2028,6 +2042,7 @@ static void bb_plan(gs_ctx *c) {
             GS_HIP(hipGetLastError());
         }
     }
+    prof_end(c, tp, "bb_plan", 0.0);
     R.planned = true;
 }
 
