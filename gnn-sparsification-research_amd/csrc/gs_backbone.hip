@@ -1502,19 +1502,13 @@ __global__ void k_bb_fill_u64(unsigned long long *p, int64_t n, unsigned long lo
 }
 
 // sources: rows with an unresolved target (other parts' columns are marked 3)
-__global__ void k_bb_need(const int64_t *__restrict__ optr, const int64_t *__restrict__ order,
-                          const uint8_t *__restrict__ state, int64_t n,
-                          int64_t *__restrict__ flag) {
-    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
-         u += (int64_t)gridDim.x * blockDim.x) {
-        int64_t f = 0;
-        for (int64_t j = optr[u]; j < optr[u + 1]; ++j)
-            if (state[order[j]] == 0) {
-                f = 1;
-                break;
-            }
-        flag[u] = f;
-    }
+// flag[u] = 1 for every row with an open column (flag zeroed before); one thread per
+// column (a thread per row walked a hub's 10^4-10^5 columns alone: 3.3 ms on RMAT-18)
+__global__ void k_bb_need(const int64_t *__restrict__ src, const uint8_t *__restrict__ state,
+                          int64_t E, int64_t *__restrict__ flag) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x)
+        if (state[i] == 0) flag[src[i]] = 1;
 }
 
 __global__ void k_bb_compact(const int64_t *__restrict__ flag, const int64_t *__restrict__ pos,
@@ -1692,6 +1686,10 @@ struct BbRun {
     int cross = 1, rev = 1;
     bool dynamic = true;
     double delta = 0.0;
+    // the search slabs hold +inf labels / zero masks between searches (every batch resets
+    // what it touched): filled only when (re)allocated or grown
+    void *dist_ok = nullptr, *q_ok = nullptr;
+    size_t dist_ok_bytes = 0, q_ok_bytes = 0;
     unsigned long long *misc = nullptr;  // [0] unique edges, [1] relaxations, [2] batch
                                          // counter, [3] debug count; misc + 4: bad flag
     hipEvent_t tall = nullptr;           // the "metric_backbone" profile region
@@ -1836,7 +1834,7 @@ static void bb_begin(gs_ctx *c, int64_t n, int64_t E, const int64_t *src, const 
             if (mine > 0 && coop) {
                 const int64_t cap = n + hgp[n] / kLmChunk + 64;  // items of one round, at most
                 uint64_t *items = (uint64_t *)c->buf("bb_lmitems").ensure(16 * (size_t)mine * cap);
-                uint32_t *stamp = (uint32_t *)b_qflag.ensure(4 * (size_t)mine * n);
+                uint32_t *stamp = (uint32_t *)c->buf("bb_lmstamp").ensure(4 * (size_t)mine * n);
                 int32_t *cnt = (int32_t *)c->buf("bb_lmcnt").ensure(16 * (size_t)mine);
                 unsigned long long *tot = R.misc + 6;
                 GS_HIP(hipMemsetAsync(stamp, 0, 4 * (size_t)mine * n, s));
@@ -1941,7 +1939,8 @@ static void bb_plan(gs_ctx *c) {
         int64_t *flag = (int64_t *)c->buf("bb_flag").ensure(8 * (n + 1));
         int64_t *pos = (int64_t *)c->buf("bb_pos").ensure(8 * (n + 1));
         hipEvent_t tq = prof_begin(c);
-        k_bb_need<<<grid_for(n, 256, 8192), 256, 0, s>>>(R.optr, R.order, R.state, n, flag);
+        GS_HIP(hipMemsetAsync(flag, 0, 8 * (n + 1), s));
+        k_bb_need<<<grid_for(E, 256, 8192), 256, 0, s>>>(R.dsrc, R.state, E, flag);
         exclusive_scan_i64(c, flag, pos, n);
         int64_t lastp = 0, lastf = 0;
         if (n) {
@@ -1995,13 +1994,24 @@ static void bb_plan(gs_ctx *c) {
             if (slabs > cap) slabs = cap;
             R.slabs = slabs;
             hipEvent_t tf = prof_begin(c);
-            R.dist = (unsigned long long *)c->buf("bb_dist").ensure(8 * (size_t)S * slabs * n);
-            R.qflag = (int32_t *)c->buf("bb_qflag").ensure(4 * slabs * n);
+            const size_t dbytes = 8 * (size_t)S * slabs * n, qbytes = 4 * (size_t)slabs * n;
+            R.dist = (unsigned long long *)c->buf("bb_dist").ensure(dbytes);
+            R.qflag = (int32_t *)c->buf("bb_qflag").ensure(qbytes);
             R.fr = (int32_t *)c->buf("bb_fr").ensure(8 * slabs * n);
             R.touched = (int32_t *)c->buf("bb_touched").ensure(4 * slabs * n);
-            k_bb_fill_u64<<<grid_for((int64_t)S * slabs * n, 256, 65536), 256, 0, s>>>(
-                R.dist, (int64_t)S * slabs * n, kInfBits);
-            GS_HIP(hipMemsetAsync(R.qflag, 0, 4 * slabs * n, s));
+            // (RMAT-18, 16 sources x 512 slabs: 17 GB, 3.2 ms per prune when filled each time)
+            const bool refill = getenv("GSPARSE_BB_REFILL") != nullptr;
+            if (refill || R.dist_ok != (void *)R.dist || R.dist_ok_bytes < dbytes) {
+                k_bb_fill_u64<<<grid_for((int64_t)S * slabs * n, 256, 65536), 256, 0, s>>>(
+                    R.dist, (int64_t)S * slabs * n, kInfBits);
+                R.dist_ok = R.dist;
+                R.dist_ok_bytes = dbytes;
+            }
+            if (refill || R.q_ok != (void *)R.qflag || R.q_ok_bytes < qbytes) {
+                GS_HIP(hipMemsetAsync(R.qflag, 0, qbytes, s));
+                R.q_ok = R.qflag;
+                R.q_ok_bytes = qbytes;
+            }
             prof_end(c, tf, "bb_plan_fill", 0.0);
             R.bt = big ? (wide ? 1024 : 512) : 256;
             if (const char *e = getenv("GSPARSE_BB_THREADS")) R.bt = atoi(e) == 1024 ? 1024 : atoi(e) == 512 ? 512 : 256;
