@@ -380,6 +380,12 @@ struct JacHashProbe {
             s.q = tab[s.h];
         }
     }
+    // the home bucket alone, branch-free: hit, or more = the search must go on (done())
+    __device__ __forceinline__ bool check1(int32_t x, S s, bool &more) const {
+        const bool hit = s.q.x == x || s.q.y == x || s.q.z == x || s.q.w == x;
+        more = !hit && s.q.w != -1;
+        return hit;
+    }
 };
 
 struct JacBitProbe {
@@ -389,6 +395,10 @@ struct JacBitProbe {
     };
     __device__ __forceinline__ S first(int32_t x) const { return S{m[x >> 5]}; }
     __device__ __forceinline__ bool done(int32_t x, S s) const { return (s.w >> (x & 31)) & 1u; }
+    __device__ __forceinline__ bool check1(int32_t x, S s, bool &more) const {
+        more = false;
+        return done(x, s);
+    }
 };
 
 // Probe phase shared by the LDS-table and bitmap kernels (after jac_stage and
@@ -404,6 +414,9 @@ struct JacBitProbe {
 // waves already.
 #ifndef GS_JAC_MASKLOAD
 #define GS_JAC_MASKLOAD 1
+#endif
+#ifndef GS_JAC_FASTPROBE
+#define GS_JAC_FASTPROBE 1
 #endif
 template <class Probe, int UL = kJacUnrollDef, int UP = UL>
 __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix, int64_t du,
@@ -437,10 +450,30 @@ __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
             typename Probe::S ps[P];
 #pragma unroll
             for (int t = 0; t < P; ++t) ps[t] = pr.first(xs[g + t] >= 0 ? xs[g + t] : 0);
+            if constexpr (GS_JAC_FASTPROBE) {
+                // the home buckets branch-free; the rare lanes whose search goes on take
+                // done() under one wave-uniform branch (a per-element search loop costs
+                // ~20 scalar mask operations per element even when it ends at once)
+                bool hit[P], more[P], any = false;
+#pragma unroll
+                for (int t = 0; t < P; ++t) {
+                    hit[t] = pr.check1(xs[g + t], ps[t], more[t]);
+                    more[t] = more[t] && xs[g + t] >= 0;
+                    any = any || more[t];
+                }
+                if (__builtin_amdgcn_ballot_w64(any)) {
+#pragma unroll
+                    for (int t = 0; t < P; ++t)
+                        if (more[t]) hit[t] = pr.done(xs[g + t], ps[t]);
+                }
+#pragma unroll
+                for (int t = 0; t < P; ++t) cnt += __popcll(__ballot(xs[g + t] >= 0 && hit[t]));
+            } else {
 #pragma unroll
             for (int t = 0; t < P; ++t) {
                 const bool hit = xs[g + t] >= 0 && pr.done(xs[g + t], ps[t]);
                 cnt += __popcll(__ballot(hit));
+            }
             }
         }
     };
@@ -482,7 +515,17 @@ __device__ __forceinline__ void jac_probe_staged(const int32_t *__restrict__ ix,
         const int64_t dv = ok ? st.dv[k] : 0;
         const int32_t x = gl < dv ? ix[st.b[k] + gl] : -1;
         const typename Probe::S ps = pr.first(x >= 0 ? x : 0);
-        const bool hit = x >= 0 && pr.done(x, ps);
+        bool hit;
+        if constexpr (GS_JAC_FASTPROBE) {
+            bool more;
+            hit = pr.check1(x, ps, more);
+            more = more && x >= 0;
+            if (__builtin_amdgcn_ballot_w64(more))
+                if (more) hit = pr.done(x, ps);
+            hit = hit && x >= 0;
+        } else {
+            hit = x >= 0 && pr.done(x, ps);
+        }
         const int64_t cnt = __popcll(__ballot(hit) & gmask);
         if (ok && gl == 0) sk.put(lo + st.off[k], cnt, du, dv);
     }
@@ -593,6 +636,13 @@ struct JacQProbe {
             s.q = tab[(home + d) & nbm];
         }
     }
+    __device__ __forceinline__ bool check1(int32_t, S s, bool &more) const {
+        const uint32_t t = (1u << p.qb) | (s.h & p.rmask), t2 = t | (t << 16);
+        const bool hit = (jac_hz16(s.q.x ^ t2) | jac_hz16(s.q.y ^ t2) | jac_hz16(s.q.z ^ t2) |
+                          jac_hz16(s.q.w ^ t2)) != 0;
+        more = !hit && (s.q.w >> 16) != 0 && p.dmax >= 1;
+        return hit;
+    }
 };
 
 // the overflow path: binary search of the owner's sorted neighbour list
@@ -601,6 +651,10 @@ struct JacSortedProbe {
     int64_t du;
     struct S {};
     __device__ __forceinline__ S first(int32_t) const { return S{}; }
+    __device__ __forceinline__ bool check1(int32_t, S, bool &more) const {
+        more = true;
+        return false;
+    }
     __device__ __forceinline__ bool done(int32_t x, S) const {
         int64_t lo = 0, hi = du;
         while (lo < hi) {
