@@ -45,12 +45,20 @@ out = {"E": int(E), "K": K, "complete": C.cpu().numpy().tolist(), "state_counts"
        "max_cost": float(big), "cost_quantiles": np.quantile(cost, [0.1, 0.5, 0.9, 0.99]).tolist(),
        "n_maxcost_cols": int((cost == big).sum()), "open_maxcost": int(((cost == big) & (s == 0)).sum()),
        "open_weight_quantiles": np.quantile(cost[s == 0], [0.1, 0.5, 0.9, 0.99]).tolist() if (s == 0).any() else []}
-idx = np.flatnonzero((cost == big) & (s == 0))[:40]
-rows = []
-for i in idx:
-    u, v = int(ei[0][i]), int(ei[1][i])
-    lb = D[u] + D[v]
-    rows.append({"u": u, "v": v, "deg_u": int(deg[u]), "deg_v": int(deg[v]), "best_landmark_path": float(lb.min()),
-                 "Du_min": float(D[u].min()), "Dv_min": float(D[v].min())})
-out["examples"] = rows
+deg = None
+# the open columns' fate: finish the prune
+nb = st.plan()
+st.search(0, nb, 0, 1)
+keep = torch.empty(E, dtype=torch.uint8, device=dev)
+st.finish(keep)
+k = keep.cpu().numpy().astype(bool)
+op = s == 0
+out["open"] = int(op.sum())
+out["open_kept"] = int((op & k).sum())
+out["open_pruned"] = int((op & ~k).sum())
+out["open_kept_weight_q"] = np.quantile(cost[op & k], [0.1, 0.5, 0.9]).tolist() if (op & k).any() else []
+out["open_pruned_weight_q"] = np.quantile(cost[op & ~k], [0.1, 0.5, 0.9]).tolist() if (op & ~k).any() else []
+out["open_kept_maxcost"] = int((op & k & (cost == big)).sum())
+out["open_pruned_maxcost"] = int((op & ~k & (cost == big)).sum())
+out["batches"] = nb
 print(json.dumps(out))
