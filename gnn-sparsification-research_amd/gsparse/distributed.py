@@ -259,10 +259,10 @@ def backbone_phases(nbatch: int, world: int, fractions=None) -> list[tuple[int, 
 
 # the ascending-count order's short searches decide most hub columns (reverse columns):
 # the ranks exchange their decisions at these fractions of the batch list (RMAT-18, one
-# rank's stages run alone, with the local-bound certificates: (0.7, 0.9) 276.6 / 173.8 /
-# 116.7 ms at N = 2 / 4 / 8 against 454.9 ms whole; (0.6, 0.9) 286.5 / 187.8 / 122.1;
-# (0.8) 281.7 / 163.8 / 118.9; tools/bb_stage_probe.py, profiles/r05u_*)
-BB_PHASES = (0.7, 0.9)
+# rank's stages run alone, with the 3- / 4-edge local bounds: (0.6, 0.85) 251.5 / 150.3 /
+# 105.0 ms at N = 2 / 4 / 8 against 407.6 ms whole; (0.7, 0.9) 262.5 / 161.1 / 108.8;
+# (0.8) 258.2 / 145.7 / 110.6; tools/bb_stage_probe.py, profiles/r05z7_*)
+BB_PHASES = (0.6, 0.85)
 BB_PHASES_4 = (0.8,)  # 4 to 7 ranks
 
 
@@ -284,9 +284,9 @@ def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
 
     `method`: "staged" (above) or "pairs" -- the round-4 split: both directions of a
     pair decided by rank max(u, v) % N in one call (gs_metric_backbone_part), one SUM
-    all-reduce of the keep bytes.  Default: "staged" (RMAT-18, a rank's work alone:
-    276.6 vs 315.9 ms at N = 2, 116.7 vs 185.4 ms at N = 8; tools/bb_stage_probe.py,
-    tools/bb_probe.py, profiles/r05u_*)."""
+    all-reduce of the keep bytes.  Default: "staged" (RMAT-18, a rank's work alone,
+    before the 3- / 4-edge bounds: 276.6 vs 315.9 ms at N = 2, 116.7 vs 185.4 ms at
+    N = 8; tools/bb_stage_probe.py, tools/bb_probe.py, profiles/r05u_*)."""
     from .metric_backbone import BackboneStages, check_weights
 
     E = (edge_index.shape[1] if not isinstance(edge_index, torch.Tensor)
