@@ -454,9 +454,14 @@ def test_backbone_rmat12_vs_oracle(gs):
 
 
 @pytest.mark.parametrize("graph", ["rmat14", "hub", "roman"])
-def test_backbone_certificates_match_plain_search(gs, graph, monkeypatch):
-    """Landmark / degree-1 certificates (default) vs the plain 2-hop witness +
-    bounded search (GSPARSE_BB_LANDMARKS=0, pinned to the oracle above)."""
+@pytest.mark.parametrize("off", [("GSPARSE_BB_LANDMARKS",), ("GSPARSE_BB_LOCALLB",),
+                                 ("GSPARSE_BB_LANDMARKS", "GSPARSE_BB_LOCALLB")])
+def test_backbone_certificates_match_plain_search(gs, graph, off, monkeypatch):
+    """Landmark / degree-1 / local-bound certificates (default) vs the search with
+    the landmark certificates, the local bounds (least other edge weights; the 3- and
+    4-edge bounds of the witness pass) or both off (GSPARSE_BB_LANDMARKS=0,
+    GSPARSE_BB_LOCALLB=0; the plain 2-hop witness + bounded search is pinned to the
+    oracle above)."""
     from gsparse import graphs
     from gsparse.metric_backbone import backbone_mask
 
@@ -468,7 +473,8 @@ def test_backbone_certificates_match_plain_search(gs, graph, monkeypatch):
         ei, n = graphs.roman_like(), 22662
     w = _column_costs(ei, n)
     keep = backbone_mask(ei, n, w)
-    monkeypatch.setenv("GSPARSE_BB_LANDMARKS", "0")
+    for var in off:
+        monkeypatch.setenv(var, "0")
     keep0 = backbone_mask(ei, n, w)
     assert np.array_equal(keep, keep0)
     assert 0 < keep.sum() < len(keep)
