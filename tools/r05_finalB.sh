@@ -11,5 +11,5 @@ for wl in rmat backbone arxiv scorers; do
 done
 timeout -k 10 300 python tools/api_timer.py > "$OUT/api_roman.json" 2> "$OUT/api_roman.err" || exit $?
 timeout -k 10 300 python tools/api_timer.py rmat > "$OUT/api_rmat.json" 2> "$OUT/api_rmat.err" || exit $?
-timeout -k 10 900 python -u tools/bb_stage_probe.py 18 "0.6,0.9;0.5,0.8,0.95;" > "$OUT/bb_stage_probe.jsonl" 2> "$OUT/bb_stage_probe.err" || { echo "probe rc=$?"; exit 1; }
+timeout -k 10 900 python -u tools/bb_stage_probe.py 18 "0.6,0.85;0.8;0.7,0.9;" > "$OUT/bb_stage_probe.jsonl" 2> "$OUT/bb_stage_probe.err" || { echo "probe rc=$?"; exit 1; }
 tail -1 "$OUT/bb_stage_probe.jsonl"
