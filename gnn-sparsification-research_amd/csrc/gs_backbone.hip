@@ -611,11 +611,16 @@ __device__ __forceinline__ void bb_block_max_s(unsigned long long (&m)[S], unsig
 // re-expands ~1.9x as many on RMAT-18's Jaccard costs; near-far ~1.05x at
 // delta = median weight / 2, tools/bb_nearfar_sim.c) -- the fixpoint, and so
 // every distance and decision, is the same in any order.
-template <int NT, int S>
+// PAIR (S = 2; the meet-in-the-middle certificate, bb_pair_certify): batch b searches
+// both ends of the open column sources[b] = i (src[i], dst[i]) to the radius
+// r = w_max (1 + 8m) / 2, w_max the larger of its and its reverse columns' weights, with
+// no target pruning, then decides the column and its reverse columns where the balls
+// prove it (see the evaluation below).
+template <int NT, int S, bool PAIR = false>
 __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     const int64_t *__restrict__ gp, const int32_t *__restrict__ gi, const double *__restrict__ gw,
     int64_t n, const int64_t *__restrict__ sources, int64_t nsrc, const int64_t *__restrict__ optr,
-    const int64_t *__restrict__ order, const int64_t *__restrict__ dst,
+    const int64_t *__restrict__ order, const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
     const double *__restrict__ w, double eps, uint8_t *__restrict__ state,
     unsigned long long *__restrict__ dist_all, uint32_t *__restrict__ qmask_all,
     int32_t *__restrict__ fr_all, uint32_t *__restrict__ fm_all, int32_t *__restrict__ touched_all,
@@ -623,8 +628,10 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     const int64_t *__restrict__ sidx, const int64_t *__restrict__ rpos, int64_t E, double mrg,
     int rev, int64_t b0, int64_t b1, int part, int nparts,
     unsigned long long *__restrict__ batch_next, unsigned long long *__restrict__ relax_total,
-    unsigned long long *__restrict__ trace) {
+    unsigned long long *__restrict__ trace, const uint8_t *__restrict__ lmflag = nullptr,
+    const double *__restrict__ LD = nullptr, const int32_t *__restrict__ lcomp = nullptr, int K = 0) {
     static_assert(S >= 1 && S <= 16, "1..16 sources per workgroup");
+    static_assert(!PAIR || S == 2, "the pair form searches both ends of one column");
     // queue bits of the per-node mask; the near-far order needs S more bits for the
     // far pile (S <= 8 only: 16 sources fill the word)
     constexpr uint32_t QS = S <= 8 ? kQMaskSources : 0xffffu;
@@ -656,7 +663,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     const double thr0 = delta > 0.0 ? delta : __longlong_as_double((long long)kInfBits);
     if (threadIdx.x == 0) s_relax = 0;
     unsigned long long relax = 0;
-    const int64_t nbatch = (nsrc + S - 1) / S;
+    const int64_t nbatch = PAIR ? nsrc : (nsrc + S - 1) / S;
+    __shared__ int64_t s_pcol;
     // batches taken in order from a global counter as workgroups free up (batch_next;
     // null: static striding), so the long searches at the end of the order do not
     // leave workgroups idle behind a fixed share
@@ -672,13 +680,36 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
         // GSPARSE_BB_TRACE: the batch's start / end on the constant clock and workgroup
         const unsigned long long tb0 = trace ? (unsigned long long)wall_clock64() : 0ull;
         if (threadIdx.x < S) {
-            const int64_t si = bi * S + threadIdx.x;
-            s_src[threadIdx.x] = si < nsrc ? sources[si] : -1;
+            if constexpr (PAIR) {
+                const int64_t i = sources[bi];
+                s_src[threadIdx.x] = threadIdx.x == 0 ? src[i] : dst[i];
+                if (threadIdx.x == 0) s_pcol = i;
+            } else {
+                const int64_t si = bi * S + threadIdx.x;
+                s_src[threadIdx.x] = si < nsrc ? sources[si] : -1;
+            }
             s_wkey[threadIdx.x] = 0ull;
             s_thr[threadIdx.x] = thr0;
             s_farmin[threadIdx.x] = kInfBits;
         }
         __syncthreads();
+        if constexpr (PAIR) {  // the radius: half the larger of the pair's open weights
+            if (threadIdx.x == 0) {
+                const int64_t i = s_pcol, u = s_src[0], v = s_src[1];
+                double wm = w[i];
+                const int64_t rp = rpos[i];
+                if (rp >= 0) {
+                    const uint64_t rkey = (uint64_t)v * (uint64_t)n + (uint64_t)u;
+                    for (int64_t p = rp; p < E && skeys[p] == rkey; ++p)  // the open ones only
+                        if (state[sidx[p]] == 0) wm = w[sidx[p]] > wm ? w[sidx[p]] : wm;
+                }
+                const double r = wm * (1.0 + 8.0 * mrg) * 0.5;
+                // an end that is a (complete) landmark: its labels are exact already
+                const bool skip = lmflag && (lmflag[u] || lmflag[v]);
+                s_wkey[0] = s_wkey[1] = skip ? 0ull : dkey(r);
+            }
+            __syncthreads();
+        } else
         // largest unresolved target weight of each source (none: nothing to decide)
         {
             unsigned long long lm[S];
@@ -828,12 +859,26 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                     uint32_t imp = 0, fimp = 0;
+                    bool btouch = false;  // PAIR: a label set beyond the radius
+                    // PAIR: complete landmarks are reached, never expanded (their labels
+                    // bound the paths through them, min_l D_l(u) + D_l(v))
+                    const bool blk = PAIR && lmflag && mm[u] && lmflag[y[u]];
 #pragma unroll
                     for (int k = 0; k < S; ++k) {
                         if (!((mm[u] >> k) & 1u)) continue;
                         ++relax;
                         const double nd = w_d[wv][lo[u]][k] + we[u];
-                        if (!(nd <= wmax_of(k))) continue;
+                        if (!(nd <= wmax_of(k)) || blk) {
+                            // PAIR: kept (a T label of the certificate), never expanded
+                            if constexpr (PAIR) {
+                                const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
+                                if (nb < cd[u][k]) {
+                                    atomicMin(&dist[(int64_t)y[u] * S + k], nb);
+                                    btouch = true;
+                                }
+                            }
+                            continue;
+                        }
                         const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
                         if (nb >= cd[u][k]) continue;
                         if (bb_min_improves(&dist[(int64_t)y[u] * S + k], nb)) {
@@ -856,6 +901,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                         if (fimp && !(om & kQMaskTouched)) touched[atomicAdd(&s_tcount, 1)] = y[u];
                         nearacc |= imp;
                     }
+                    if (PAIR && btouch && !(atomicOr(&qmask[y[u]], kQMaskTouched) & kQMaskTouched))
+                        touched[atomicAdd(&s_tcount, 1)] = y[u];
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -886,12 +933,23 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                                                                         __HIP_MEMORY_SCOPE_WORKGROUP)
                                                     : 0ull;
                         uint32_t imp = 0, fimp = 0;
+                        bool btouch = false;
+                        const bool blk = PAIR && lmflag && lmflag[y];
 #pragma unroll
                         for (int k = 0; k < S; ++k) {
                             if (!((m >> k) & 1u)) continue;
                             ++relax;
                             const double nd = w_d[0][0][k] + we;
-                            if (!(nd <= wmax_of(k))) continue;
+                            if (!(nd <= wmax_of(k)) || blk) {
+                                if constexpr (PAIR) {
+                                    const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
+                                    if (nb < cd[k]) {
+                                        atomicMin(&dist[(int64_t)y * S + k], nb);
+                                        btouch = true;
+                                    }
+                                }
+                                continue;
+                            }
                             const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
                             if (nb >= cd[k]) continue;
                             if (bb_min_improves(&dist[(int64_t)y * S + k], nb)) {
@@ -911,6 +969,8 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                             if (fimp && !(om & kQMaskTouched)) touched[atomicAdd(&s_tcount, 1)] = y;
                             nearacc |= imp;
                         }
+                        if (PAIR && btouch && !(atomicOr(&qmask[y], kQMaskTouched) & kQMaskTouched))
+                            touched[atomicAdd(&s_tcount, 1)] = y;
                     }
                     __syncthreads();
                 }
@@ -943,7 +1003,10 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
             // hook: prune targets per source, lower its bound, end when all are done
             if (threadIdx.x < S) s_wkey[threadIdx.x] = 0ull;
             __syncthreads();
-            {
+            if constexpr (PAIR) {
+                if (threadIdx.x < S) s_wkey[threadIdx.x] = dkey(s_wmax[threadIdx.x]);  // the radius stays
+                __syncthreads();
+            } else {
                 unsigned long long mx[S];
 #pragma unroll
                 for (int k = 0; k < S; ++k) {
@@ -1036,6 +1099,100 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                 __syncthreads();
             }
         }
+        if constexpr (PAIR) {
+            // The balls of radius r around u and v (labels <= r exact, expanded; a label
+            // beyond r is kept but never expanded: T_v(x) = min over v's ball nodes y of
+            // d_v(y) + w_yx, the fold of a real v-x walk).  Every u-v path P but the edge
+            // itself, of length L <= 2r (1 - 3m): x = its last node with
+            // d_P(u, x) <= r (1 - 2m) and y the next lie in u's and v's balls (the labels
+            // fold within m of the exact lengths; d_P(y, v) < r (1 - 4m)), so
+            // d_u(x) + T_v(x) <= L (1 + 2m) (x = v: T_v(v) = 0).  x = u (P's first edge
+            // leaves u's ball) is taken over u's other edges: w_uy + d_v(y), y in v's ball.
+            // So M = min(min over x in u's ball but u of d_u(x) + T_v(x),
+            //            min over (u, y), y != v, d_v(y) <= r of w_uy + d_v(y))
+            // is at most (1 + 4m) times every such path's fold; every term is the length of
+            // a real u-v walk (one through the edge itself is at least w_G: the prune below
+            // then follows from d <= w_G; x = u, whose T_v may hold w_G, is excluded).  A
+            // column (u, v) or (v, u) of weight w <= 2r (1 - 5m) (a longer path folds to
+            // more than 2r (1 - 4m) > w):
+            //  * w > fl(w_G + eps) (its own edge in G is shorter): prune (d <= w_G);
+            //  * M (1 - 5m) >= w: every alternative path folds to >= w, and w <=
+            //    fl(w_G + eps): keep (the reference's w <= fl(d + eps));
+            //  * (M (1 + 4m) + eps)(1 + m) < w: a shorter path exists: prune.
+            // Otherwise the column stays open for the searches.
+            const int64_t u = s_src[0], v = s_src[1];
+            const double r = s_wmax[0];
+            double mloc = __longlong_as_double((long long)kInfBits);
+            // paths through a blocked landmark l: at least D_l(u) + D_l(v) (its exact labels)
+            if (lmflag)
+                for (int l = threadIdx.x; l < K; l += NT)
+                    if (lcomp[l]) {
+                        const double t2 = (LD[u * K + l] + LD[v * K + l]) * (1.0 - 2.0 * mrg);
+                        mloc = t2 < mloc ? t2 : mloc;
+                    }
+            const int tc = s_tcount;
+            for (int t = threadIdx.x; t < tc; t += NT) {
+                const int32_t x = touched[t];
+                if (x == (int32_t)u) continue;  // u's first edges: below
+                const double du = __longlong_as_double((long long)__hip_atomic_load(
+                    &dist[(int64_t)x * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                const unsigned long long bv = __hip_atomic_load(&dist[(int64_t)x * 2 + 1], __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (du <= r && bv != kInfBits) {
+                    const double t2 = du + __longlong_as_double((long long)bv);
+                    mloc = t2 < mloc ? t2 : mloc;
+                }
+            }
+            for (int64_t e = gp[u] + threadIdx.x; e < gp[u + 1]; e += NT) {
+                const int32_t y = gi[e];
+                if (y == (int32_t)v) continue;
+                const double dv = __longlong_as_double((long long)__hip_atomic_load(
+                    &dist[(int64_t)y * 2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (dv <= r) {
+                    const double t2 = gw[e] + dv;
+                    mloc = t2 < mloc ? t2 : mloc;
+                }
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                const double o = __shfl_xor(mloc, off, 64);
+                mloc = o < mloc ? o : mloc;
+            }
+            if ((threadIdx.x & 63) == 0)  // mloc >= 0: its bits order as the values
+                atomicMin(&s_amin, (unsigned long long)__double_as_longlong(mloc));
+            __syncthreads();
+            if (threadIdx.x == 0 && r >= 0.0) {
+                const double M = __longlong_as_double((long long)s_amin);
+                // w_G(u, v): v in the shorter of the two sorted lists
+                const int64_t du = gp[u + 1] - gp[u], dvv = gp[v + 1] - gp[v];
+                const bool us = du <= dvv;
+                int64_t lo = us ? gp[u] : gp[v], hi = us ? gp[u + 1] : gp[v + 1];
+                const int64_t end = hi;
+                const int32_t key = (int32_t)(us ? v : u);
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    if (gi[mid] < key) lo = mid + 1;
+                    else hi = mid;
+                }
+                const bool has = lo < end && gi[lo] == key;
+                const double wg = has ? gw[lo] : 0.0;
+                auto decide = [&](int64_t c) {
+                    if (state[c] != 0) return;
+                    const double wc = w[c];
+                    if (!(wc <= 2.0 * r * (1.0 - 5.0 * mrg))) return;
+                    if (has && wc > wg + eps) state[c] = 2;
+                    else if (M * (1.0 - 5.0 * mrg) >= wc) state[c] = 1;
+                    else if ((M * (1.0 + 4.0 * mrg) + eps) * (1.0 + mrg) < wc) state[c] = 2;
+                };
+                decide(s_pcol);
+                const int64_t rp = rpos[s_pcol];
+                if (rp >= 0) {
+                    const uint64_t rkey = (uint64_t)v * (uint64_t)n + (uint64_t)u;
+                    for (int64_t p = rp; p < E && skeys[p] == rkey; ++p) decide(sidx[p]);
+                }
+            }
+            if (threadIdx.x == 0) s_amin = kInfBits;
+            __syncthreads();
+        } else {
         // classify each source's unresolved targets; with cross != 0 also the reverse
         // columns (v, u) still open, from u's label of v (bb_cross_decide)
         for (int k = 0; k < S; ++k) {
@@ -1102,6 +1259,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                 __syncthreads();
             }
         }
+        }  // !PAIR
         __syncthreads();
         if (trace && relax != relax0) atomicAdd(&trace[6 * bj + 5], relax - relax0);
         const int tc = s_tcount;
@@ -1750,6 +1908,7 @@ struct BbRun {
     uint64_t *skeys = nullptr;
     int64_t *sidx = nullptr, *rpos = nullptr;
     int cross = 1, rev = 1;
+    bool keys_ready = false;  // skeys / sidx / rpos built for this run
     bool dynamic = true;
     double delta = 0.0;
     // the search slabs hold +inf labels / zero masks between searches (every batch resets
@@ -1783,6 +1942,7 @@ static void bb_begin(gs_ctx *c, int64_t n, int64_t E, const int64_t *src, const 
     GS_HIP(hipSetDevice(c->device));
     BbRun &R = bb_run(c);
     R.begun = R.certified = R.planned = false;
+    R.keys_ready = false;
     R.n = n;
     R.E = E;
     R.eps = eps;
@@ -1953,6 +2113,55 @@ static void bb_begin(gs_ctx *c, int64_t n, int64_t E, const int64_t *src, const 
     R.begun = true;
 }
 
+// every column's (row * n + col) key sorted, its column, and the position of its reverse
+// key (the reverse-column decisions of the searches and the pair certificate); once per run
+static void bb_keys(gs_ctx *c) {
+    BbRun &R = bb_run(c);
+    if (R.keys_ready) return;
+    hipStream_t s = c->stream;
+    const int64_t E = R.E, n = R.n;
+    R.skeys = (uint64_t *)c->buf("bb_skeys").ensure(8 * E);
+    R.sidx = (int64_t *)c->buf("bb_sidx").ensure(8 * E);
+    R.rpos = (int64_t *)c->buf("bb_rpos").ensure(8 * E);
+    k_bb_pairkeys<<<grid_for(E, 256, 8192), 256, 0, s>>>(R.dsrc, R.ddst, E, n, R.skeys, R.sidx);
+    sort_pairs_u64_i64(c, R.skeys, R.sidx, E, bits_for_bb((uint64_t)n * (uint64_t)n));
+    k_bb_revpos<<<grid_for(E, 256, 8192), 256, 0, s>>>(R.dsrc, R.ddst, E, n, R.skeys, R.rpos);
+    GS_HIP(hipGetLastError());
+    R.keys_ready = true;
+}
+
+// the pair certificate's columns in [c0, c1): open, not a self-loop, one of each
+// (u, v) / (v, u) pair (the u < v one when both are open)
+__global__ void k_bb_pairflag(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
+                              const uint8_t *__restrict__ state, const int64_t *__restrict__ rpos,
+                              const int64_t *__restrict__ sidx, int64_t c0, int64_t c1,
+                              int64_t *__restrict__ flag) {
+    for (int64_t i = c0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < c1;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t u = src[i], v = dst[i];
+        int64_t f = 0;
+        if (state[i] == 0 && u != v) {
+            const int64_t rp = rpos[i];
+            f = (u < v || rp < 0 || state[sidx[rp]] != 0) ? 1 : 0;
+        }
+        flag[i - c0] = f;
+    }
+}
+
+// lmflag[x] = 1 for the complete landmarks (k_bb_sssp_multi PAIR does not expand them)
+__global__ void k_bb_lmflag(const int32_t *__restrict__ lm, const int32_t *__restrict__ lcomp, int K,
+                            uint8_t *__restrict__ lmflag) {
+    for (int l = threadIdx.x; l < K; l += blockDim.x)
+        if (lcomp[l]) lmflag[lm[l]] = 1;
+}
+
+__global__ void k_bb_pcompact(const int64_t *__restrict__ flag, const int64_t *__restrict__ pos,
+                              int64_t c0, int64_t cnt, int64_t *__restrict__ out) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < cnt;
+         j += (int64_t)gridDim.x * blockDim.x)
+        if (flag[j]) out[pos[j]] = c0 + j;
+}
+
 // witness + certificates of columns [E part / nparts, E (part + 1) / nparts)
 static void bb_certify(gs_ctx *c, int part, int nparts) {
     BbRun &R = bb_run(c);
@@ -1989,6 +2198,103 @@ static void bb_certify(gs_ctx *c, int part, int nparts) {
         k_bb_witness<<<grid_for(c1 - c0, 256, 8192), 256, 0, s>>>(
             R.dsrc, R.ddst, R.dw, c0, c1, R.gp, R.gi, R.gw, R.eps, R.pair_part, R.pair_nparts, mw, ma,
             aw, aa, mrg, R.state);
+        // the meet-in-the-middle certificate of the columns still open (k_bb_sssp_multi
+        // PAIR: both ends searched to half the column's weight; GSPARSE_BB_MITM=1: on).
+        // It needs the local bounds' direct-edge rule, so it runs only with them.  Off by
+        // default: on R-MAT-18 it decides all but 202 of the 204 k open columns, but the
+        // balls of radius ~9 around their (hub-adjacent) ends already hold ~0.28 E
+        // relaxations each -- 1.2·10¹¹ for the 102 k pairs, 3.3 s against 0.38 s for the
+        // searches it replaces (profiles/r05z10_*).
+        bool mitm = false;
+        if (const char *e = getenv("GSPARSE_BB_MITM")) mitm = local && atoi(e) != 0;
+        if (mitm) {
+            hipEvent_t tq = prof_begin(c);
+            bb_keys(c);
+            const int64_t nc = c1 - c0;
+            int64_t *pf = (int64_t *)c->buf("bb_pflag").ensure(8 * (nc + 1));
+            int64_t *pp = (int64_t *)c->buf("bb_ppos").ensure(8 * (nc + 1));
+            k_bb_pairflag<<<grid_for(nc, 256, 8192), 256, 0, s>>>(R.dsrc, R.ddst, R.state, R.rpos, R.sidx, c0,
+                                                                   c1, pf);
+            exclusive_scan_i64(c, pf, pp, nc);
+            int64_t lastp = 0, lastf = 0;
+            GS_HIP(hipMemcpyAsync(&lastp, pp + nc - 1, 8, hipMemcpyDeviceToHost, s));
+            GS_HIP(hipMemcpyAsync(&lastf, pf + nc - 1, 8, hipMemcpyDeviceToHost, s));
+            GS_HIP(hipStreamSynchronize(s));
+            const int64_t np = lastp + lastf;
+            if (getenv("GSPARSE_BB_DEBUG"))
+                fprintf(stderr, "[backbone] pair certificate: %lld open pairs\n", (long long)np);
+            if (np > 0) {
+                int64_t *plist = (int64_t *)c->buf("bb_plist").ensure(8 * np);
+                k_bb_pcompact<<<grid_for(nc, 256, 8192), 256, 0, s>>>(pf, pp, c0, nc, plist);
+                int64_t P = 512;
+                if (const char *e = getenv("GSPARSE_BB_MITM_SLABS")) P = atoi(e) > 0 ? atoi(e) : P;
+                P = std::min<int64_t>(P, np);
+                const int64_t cap = (int64_t)(48e9 / (44.0 * (double)R.n));  // slab bytes per node: 2 x 8 + 28
+                if (P > cap) P = std::max<int64_t>(cap, 1);
+                const size_t dbytes = 16 * (size_t)P * R.n, qbytes = 4 * (size_t)P * R.n;
+                auto *dist = (unsigned long long *)c->buf("bb_dist").ensure(dbytes);
+                auto *qm = (uint32_t *)c->buf("bb_qflag").ensure(qbytes);
+                auto *fr = (int32_t *)c->buf("bb_fr").ensure(8 * (size_t)P * R.n);
+                auto *fm = (uint32_t *)c->buf("bb_fmask").ensure(4 * (size_t)P * R.n);
+                auto *tch = (int32_t *)c->buf("bb_touched").ensure(4 * (size_t)P * R.n);
+                auto *farl = (int32_t *)c->buf("bb_far").ensure(8 * (size_t)P * R.n);
+                if (R.dist_ok != (void *)dist || R.dist_ok_bytes < dbytes) {
+                    k_bb_fill_u64<<<grid_for((int64_t)(dbytes / 8), 256, 65536), 256, 0, s>>>(
+                        dist, (int64_t)(dbytes / 8), kInfBits);
+                    R.dist_ok = dist;
+                    R.dist_ok_bytes = dbytes;
+                }
+                if (R.q_ok != (void *)qm || R.q_ok_bytes < qbytes) {
+                    GS_HIP(hipMemsetAsync(qm, 0, qbytes, s));
+                    R.q_ok = qm;
+                    R.q_ok_bytes = qbytes;
+                }
+                double nfs = 2.0;
+                if (const char *e = getenv("GSPARSE_BB_NEARFAR")) nfs = atof(e);
+                const double delta = nfs > 0.0 && R.wmed > 0.0 ? nfs * R.wmed : 0.0;
+                unsigned long long *bnext = R.misc + 2;
+                GS_HIP(hipMemsetAsync(bnext, 0, 8, s));
+                // complete landmarks blocked (GSPARSE_BB_MITM_LM=0: expanded like any node)
+                uint8_t *lmf = nullptr;
+                bool lmb = R.K > 0;
+                if (const char *e = getenv("GSPARSE_BB_MITM_LM")) lmb = lmb && atoi(e) != 0;
+                if (lmb) {
+                    lmf = (uint8_t *)c->buf("bb_lmflag").ensure((size_t)R.n);
+                    GS_HIP(hipMemsetAsync(lmf, 0, (size_t)R.n, s));
+                    k_bb_lmflag<<<1, 64, 0, s>>>((const int32_t *)c->buf("bb_lm").ptr, R.lcomp, R.K, lmf);
+                }
+                // GSPARSE_BB_TRACE: as bb_search's, one line per launch ("pairs": true)
+                const char *tpath = getenv("GSPARSE_BB_TRACE");
+                unsigned long long *trace = nullptr;
+                if (tpath) {
+                    trace = (unsigned long long *)c->buf("bb_trace").ensure(48 * (size_t)np);
+                    GS_HIP(hipMemsetAsync(trace, 0, 48 * (size_t)np, s));
+                }
+                k_bb_sssp_multi<512, 2, true><<<(unsigned)P, 512, 0, s>>>(
+                    R.gp, R.gi, R.gw, R.n, plist, np, R.optr, R.order, R.dsrc, R.ddst, R.dw, R.eps, R.state,
+                    dist, qm, fr, fm, tch, farl, delta, 0, R.skeys, R.sidx, R.rpos, R.E, mrg, 0, 0, np, 0, 1,
+                    bnext, R.misc + 1, trace, lmf, R.D, R.lcomp, R.K);
+                GS_HIP(hipGetLastError());
+                if (tpath) {
+                    std::vector<unsigned long long> h(6 * (size_t)np);
+                    GS_HIP(hipMemcpyAsync(h.data(), trace, 48 * (size_t)np, hipMemcpyDeviceToHost, s));
+                    GS_HIP(hipStreamSynchronize(s));
+                    if (FILE *f = fopen(tpath, "a")) {
+                        fprintf(f, "{\"pairs\": true, \"part\": %d, \"nparts\": %d, \"b0\": 0, \"b1\": %lld, \"S\": 2, \"grid\": %lld, \"rec\": [",
+                                part, nparts, (long long)np, (long long)P);
+                        for (int64_t i = 0; i < np; ++i) {
+                            double bm;
+                            memcpy(&bm, &h[6 * i + 3], 8);
+                            fprintf(f, "%s[%llu, %llu, %llu, %.9g, %llu, %llu]", i ? ", " : "", h[6 * i], h[6 * i + 1],
+                                    h[6 * i + 2], bm, h[6 * i + 4], h[6 * i + 5]);
+                        }
+                        fprintf(f, "]}\n");
+                        fclose(f);
+                    }
+                }
+            }
+            prof_end(c, tq, "bb_pairs", 0.0);
+        }
         GS_HIP(hipGetLastError());
     }
     prof_end(c, tp, "bb_certify", 0.0);
@@ -2090,17 +2396,8 @@ static void bb_plan(gs_ctx *c) {
                 // reverse-column decisions after every search (GSPARSE_BB_CROSS=0: off)
                 R.cross = 1;
                 if (const char *e = getenv("GSPARSE_BB_CROSS")) R.cross = atoi(e) != 0;
-                R.skeys = nullptr;
-                R.sidx = R.rpos = nullptr;
                 hipEvent_t tc = prof_begin(c);
-                if (R.cross) {
-                    R.skeys = (uint64_t *)c->buf("bb_skeys").ensure(8 * E);
-                    R.sidx = (int64_t *)c->buf("bb_sidx").ensure(8 * E);
-                    R.rpos = (int64_t *)c->buf("bb_rpos").ensure(8 * E);
-                    k_bb_pairkeys<<<grid_for(E, 256, 8192), 256, 0, s>>>(R.dsrc, R.ddst, E, n, R.skeys, R.sidx);
-                    sort_pairs_u64_i64(c, R.skeys, R.sidx, E, bits_for_bb((uint64_t)n * (uint64_t)n));
-                    k_bb_revpos<<<grid_for(E, 256, 8192), 256, 0, s>>>(R.dsrc, R.ddst, E, n, R.skeys, R.rpos);
-                }
+                if (R.cross) bb_keys(c);
                 prof_end(c, tc, "bb_plan_cross", 0.0);
                 // sources by ascending column count (the batches from the last): the
                 // short searches first, so their reverse-column decisions close most of
@@ -2159,7 +2456,7 @@ static void bb_search(gs_ctx *c, int64_t b0, int64_t b1, int part, int nparts) {
         }
 #define GS_BBM(NT_, S_)                                                                          \
     k_bb_sssp_multi<NT_, S_><<<grid, NT_, 0, s>>>(R.gp, R.gi, R.gw, R.n, R.sources, R.nsrc, R.optr, \
-                                                   R.order, R.ddst, R.dw, R.eps, R.state, R.dist,  \
+                                                   R.order, R.dsrc, R.ddst, R.dw, R.eps, R.state, R.dist,  \
                                                    qm, R.fr, R.fm, R.touched, R.farl, R.delta,     \
                                                    R.cross, R.skeys, R.sidx, R.rpos, R.E, mrg,     \
                                                    R.rev, b0, b1, part, nparts, bnext, R.misc + 1, \

@@ -454,14 +454,16 @@ def test_backbone_rmat12_vs_oracle(gs):
 
 
 @pytest.mark.parametrize("graph", ["rmat14", "hub", "roman"])
-@pytest.mark.parametrize("off", [("GSPARSE_BB_LANDMARKS",), ("GSPARSE_BB_LOCALLB",),
+@pytest.mark.parametrize("off", [("GSPARSE_BB_LANDMARKS",), ("GSPARSE_BB_LOCALLB",), ("+GSPARSE_BB_MITM",),
+                                 ("+GSPARSE_BB_MITM", "GSPARSE_BB_MITM_LM"),
                                  ("GSPARSE_BB_LANDMARKS", "GSPARSE_BB_LOCALLB")])
 def test_backbone_certificates_match_plain_search(gs, graph, off, monkeypatch):
-    """Landmark / degree-1 / local-bound certificates (default) vs the search with
-    the landmark certificates, the local bounds (least other edge weights; the 3- and
-    4-edge bounds of the witness pass) or both off (GSPARSE_BB_LANDMARKS=0,
-    GSPARSE_BB_LOCALLB=0; the plain 2-hop witness + bounded search is pinned to the
-    oracle above)."""
+    """Landmark / degree-1 / local-bound certificates (default) vs the search with the
+    landmark certificates, the local bounds (least other edge weights; the 3- and 4-edge
+    bounds of the witness pass) or both off, and with the pair (meet-in-the-middle)
+    certificate on, its landmarks blocked or not (GSPARSE_BB_LANDMARKS=0,
+    GSPARSE_BB_LOCALLB=0, GSPARSE_BB_MITM=1, GSPARSE_BB_MITM_LM=0; the plain 2-hop
+    witness + bounded search is pinned to the oracle above)."""
     from gsparse import graphs
     from gsparse.metric_backbone import backbone_mask
 
@@ -473,8 +475,8 @@ def test_backbone_certificates_match_plain_search(gs, graph, off, monkeypatch):
         ei, n = graphs.roman_like(), 22662
     w = _column_costs(ei, n)
     keep = backbone_mask(ei, n, w)
-    for var in off:
-        monkeypatch.setenv(var, "0")
+    for var in off:  # "+NAME": on (the pair certificate is off by default), else off
+        monkeypatch.setenv(var.lstrip("+"), "1" if var.startswith("+") else "0")
     keep0 = backbone_mask(ei, n, w)
     assert np.array_equal(keep, keep0)
     assert 0 < keep.sum() < len(keep)
@@ -1005,3 +1007,31 @@ def test_backbone_reverse_columns_vs_oracle(gs, weights, order, S, monkeypatch):
     for eps in (1e-9, 0.0):
         ref = O.metric_backbone(ei, n, w, epsilon=eps)
         assert np.array_equal(backbone_mask(ei, n, w, epsilon=eps), ref), (weights, order, eps)
+
+
+@pytest.mark.parametrize("weights", ["ties", "scales", "asymmetric"])
+def test_backbone_pair_certificate_vs_oracle(gs, weights, monkeypatch):
+    """The meet-in-the-middle certificate (k_bb_sssp_multi PAIR, GSPARSE_BB_MITM=1: both
+    ends of every open column searched to half its weight, the u-ball's labels plus the
+    v-search's labels bounding every alternative path, the direct edge's walks excluded)
+    on the margin-stressing weights of the test above, against the oracle's Dijkstra."""
+    from gsparse import graphs
+    from gsparse.metric_backbone import backbone_mask
+
+    monkeypatch.setenv("GSPARSE_BB_MITM", "1")
+    rng = np.random.default_rng(11)
+    ei, n = graphs.rmat(12, 8, seed=6), 1 << 12
+    E = ei.shape[1]
+    key = np.minimum(ei[0], ei[1]) * n + np.maximum(ei[0], ei[1])
+    _, inv = np.unique(key, return_inverse=True)
+    if weights == "ties":
+        pw = rng.integers(1, 4, size=inv.max() + 1).astype(np.float64)
+    else:
+        pw = 10.0 ** rng.uniform(-9, 9, size=inv.max() + 1)
+    w = pw[inv]
+    if weights == "asymmetric":
+        flip = rng.random(E) < 0.3
+        w = np.where(flip, w * rng.uniform(0.5, 2.0, size=E), w)
+    for eps in (1e-9, 0.0):
+        ref = O.metric_backbone(ei, n, w, epsilon=eps)
+        assert np.array_equal(backbone_mask(ei, n, w, epsilon=eps), ref), (weights, eps)
