@@ -196,3 +196,23 @@ def test_bench_refuses_more_gpus_than_visible():
                             if k not in ("WORLD_SIZE", "GSPARSE_REHEARSE")})
     assert r.returncode != 0
     assert "needs 2 GPUs" in (r.stderr + r.stdout)
+
+
+def test_backbone_phases_cut_the_batch_list(monkeypatch):
+    """gsparse.distributed.backbone_phases: one range on one rank; the default cuts at
+    BB_PHASES (BB_PHASES_4 at 4-7 ranks) of the batch list; $GSPARSE_BB_PHASES and an
+    explicit list override them; the ranges tile [0, nbatch) in order."""
+    from gsparse.distributed import BB_PHASES, BB_PHASES_4, backbone_phases
+
+    monkeypatch.delenv("GSPARSE_BB_PHASES", raising=False)
+    assert backbone_phases(1000, 1) == [(0, 1000)]
+    assert backbone_phases(0, 8) == [(0, 0)]
+    for world, fr in ((2, BB_PHASES), (3, BB_PHASES), (4, BB_PHASES_4), (7, BB_PHASES_4), (8, BB_PHASES)):
+        rng = backbone_phases(1000, world)
+        assert [b for _, b in rng[:-1]] == [int(round(f * 1000)) for f in fr]
+        assert rng[0][0] == 0 and rng[-1][1] == 1000
+        assert all(a1 == b0 for (_, a1), (b0, _) in zip(rng, rng[1:]))
+    assert backbone_phases(1000, 8, []) == [(0, 1000)]
+    assert backbone_phases(1000, 8, [0.25, 0.5]) == [(0, 250), (250, 500), (500, 1000)]
+    monkeypatch.setenv("GSPARSE_BB_PHASES", "0.5")
+    assert backbone_phases(1000, 2) == [(0, 500), (500, 1000)]
