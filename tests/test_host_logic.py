@@ -216,3 +216,28 @@ def test_backbone_phases_cut_the_batch_list(monkeypatch):
     assert backbone_phases(1000, 8, [0.25, 0.5]) == [(0, 250), (250, 500), (500, 1000)]
     monkeypatch.setenv("GSPARSE_BB_PHASES", "0.5")
     assert backbone_phases(1000, 2) == [(0, 500), (500, 1000)]
+
+
+def test_counter_join_skips_first_call_kernels():
+    """bench.kernel_counters: the profiled run has one call of the region; the Jaccard
+    plan kernels (launched by the first call on a graph only) are left out of the per-call
+    counters joined to the timed steps, and named."""
+    import importlib.util
+    import os
+
+    root = os.path.join(os.path.dirname(__file__), "..")
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    summ = {"_meta": {"calls_per_run": 1},
+            "gs::k_jac_plan(long const*)": {"launches": 1, "FETCH_SIZE_KB_per_launch": 100.0,
+                                            "WRITE_SIZE_KB_per_launch": 10.0},
+            "void gs::k_jac_hashq<32768, 1024, 8>(long const*)": {
+                "launches": 2, "FETCH_SIZE_KB_per_launch": 7.0, "WRITE_SIZE_KB_per_launch": 1.0},
+            "gs::k_bb_keep(long const*)": {"launches": 1, "FETCH_SIZE_KB_per_launch": 5.0,
+                                          "WRITE_SIZE_KB_per_launch": 5.0}}
+    c = b.kernel_counters(summ, "jaccard", 1.0)
+    assert c["FETCH_SIZE_KB"] == 14.0 and c["WRITE_SIZE_KB"] == 2.0 and c["kernels"] == 1
+    assert c["first_call_only"] == ["gs::k_jac_plan"]
+    bb = b.kernel_counters(summ, "metric_backbone", 1.0)
+    assert bb["FETCH_SIZE_KB"] == 5.0 and bb["first_call_only"] == []
