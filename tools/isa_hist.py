@@ -72,9 +72,11 @@ def main() -> None:
         cur[classify(op)] += 1
         ops[op] += 1
     phases.append(cur)
-    # iteration phases: the clock reads are (prologue) | lap(4) | p | lap(0) | spmv | lap(1) |
-    # finish | lap(2) | r update | lap(3) | finish + next column ...
-    names = ["prologue", "p_update", "spmv_pq", "finish_pq", "r_update_rr", "finish_rr_and_rest"]
+    # clock reads: tmark = wall_clock64() | column setup (r = b, b.b finish) | lap(4) |
+    # p update | lap(0) | SpMV + p.q chains | lap(1) | finish | lap(2) | r update (SpMV
+    # again) + r.r chains | lap(3) | finish + the column epilogue
+    names = ["prologue", "column_setup", "p_update", "spmv_pq", "finish_pq", "r_update_rr",
+             "finish_rr_and_rest"]
     out = {"kernel": sym, "source": path, "phases": {}}
     for i, c in enumerate(phases):
         nm = names[i] if i < len(names) else f"segment{i}"
