@@ -1158,11 +1158,24 @@ def main():
             info = {"cut": cut, "beyond": nb, "tied": nt}
         sel_info.update(info)
 
+    own_scores = None
+    if world > 1 and with_topk:
+        from gsparse.distributed import sharded_jaccard_topk
+
+        _, oo = eng.jaccard_shares(world)
+        own_scores = torch.empty(max(1, int(oo[rank + 1] - oo[rank])), dtype=torch.float64, device=dev)
+
     def step():
+        if world > 1 and with_topk:
+            # Jaccard-T over ranks without the score exchange: own owner-pair counts and
+            # scores, the cut by radix select over all-reduced histograms, one keep byte per
+            # pair all-gathered, the whole mask on every rank (gs_jsel_*)
+            _, info, _ = sharded_jaccard_topk(eng, comm, args.keep, tie_break="stable",
+                                              mask_out=mask_out, scores_out=own_scores)
+            sel_info.update(info)
+            return own_scores, None
         if world > 1:
             jac = sharded_edge_scores(eng, comm, "jaccard", bounds=bounds, out=jac_out)
-            if with_topk:
-                select(jac)
             er = sharded_approx_er(eng, comm, blas_threads=args.blas_threads,
                                    rng_mode=args.rng) if with_er else None
             return jac, er
@@ -1246,7 +1259,8 @@ def main():
         "config": {"workload": wl, "n": n, "E": E, "jl_k": k if with_er else None,
                    "cg_maxiter": 500 if with_er else None,
                    "blas_threads_order": args.blas_threads, "rng": args.rng,
-                   "parallelism": f"edges+jl-columns/{world}" if world > 1 else "1 GPU",
+                   "parallelism": ((f"owner-pair shares/{world} + histogram all-reduce select"
+                                    if with_topk else f"edges+jl-columns/{world}") if world > 1 else "1 GPU"),
                    "topk": ({"keep": args.keep, "num_keep": int(E * args.keep), "tie_rule": "device (stable)",
                              "tied_at_cut": sel_info.get("tied"), "beyond_cut": sel_info.get("beyond")}
                             if with_topk else None),

@@ -46,6 +46,35 @@ static constexpr int kQMaskFarShift = 8;
 static constexpr int64_t kBbHeavy = GS_BB_HEAVY;
 static constexpr int kBbHeavyMax = 256;
 
+// Which rule decided a column (gs_bb_classes / gs_bb_class_counts; include/gsparse.h
+// GS_BB_WHY_*).  Recorded only when the caller asks (why != null): a diagnostic for the
+// parity tests, which assert that every certificate class fires on their graphs.
+enum : uint8_t {
+    kWhyOpen = 0,      // not decided by this rank
+    kWhySelf,          // self-loop: d(u, u) = 0
+    kWhyIsolated,      // an endpoint without G edges: d = inf, keep
+    kWhyDeg1,          // an endpoint of degree 1 whose only neighbour is the other: d = w_G
+    kWhyDirect,        // w > fl(w_G + eps): prune
+    kWhyLocal2,        // w <= fl(mu' + mv')(1 - 2m): keep
+    kWhyLmComp,        // a complete landmark reaches one endpoint only: keep
+    kWhyLmPrune,       // landmark upper bound: prune
+    kWhyLmKeep,        // landmark lower bound: keep
+    kWhyWitness,       // 2-hop path: prune
+    kWhyLocal34,       // 2- / 3- / 4-edge local lower bound: keep
+    kWhySearchPrune,   // the row's search: prune
+    kWhySearchKeep,    // the row's search: keep
+    kWhyRevExact,      // the reverse row's search, exact rule
+    kWhyRevPrune,      // the reverse row's search, upper bound: prune
+    kWhyRevKeep,       // the reverse row's search, v unreached within the bound: keep
+    kWhyMitm,          // meet-in-the-middle certificate (GSPARSE_BB_MITM)
+    kWhyClasses
+};
+__device__ __forceinline__ void bb_set(uint8_t *__restrict__ state, uint8_t *__restrict__ why, int64_t i,
+                                       uint8_t st, uint8_t cls) {
+    state[i] = st;
+    if (why) why[i] = cls;
+}
+
 // osrc/odst: the caller's ids (which columns are s < d: metric_backbone.py:70-79
 // builds G from those); src/dst: the (possibly relabeled) ids G is built in
 __global__ void k_bb_keys(const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
@@ -152,7 +181,7 @@ __global__ void k_bb_witness(const int64_t *__restrict__ src, const int64_t *__r
                              const double *__restrict__ gw, double eps, int part, int nparts,
                              const double *__restrict__ mw, const int32_t *__restrict__ ma,
                              const double *__restrict__ aw, const int32_t *__restrict__ aa,
-                             double m, uint8_t *__restrict__ state) {
+                             double m, uint8_t *__restrict__ state, uint8_t *__restrict__ why) {
     for (int64_t i = c0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < c1;
          i += (int64_t)gridDim.x * blockDim.x) {
         int64_t u = src[i], v = dst[i];
@@ -163,14 +192,15 @@ __global__ void k_bb_witness(const int64_t *__restrict__ src, const int64_t *__r
         if (state[i] != 0) continue;  // decided by k_bb_certify (it runs first)
         double wi = w[i];
         if (u == v) {  // d(u,u) = 0
-            state[i] = (wi <= 0.0 + eps) ? 1 : 2;
+            bb_set(state, why, i, (wi <= 0.0 + eps) ? 1 : 2, kWhySelf);
             continue;
         }
         int64_t a = gp[u], ae = gp[u + 1], b = gp[v], be = gp[v + 1];
-        uint8_t st = 0;
+        uint8_t st = 0, cls = kWhyOpen;
         double w2 = __builtin_inf();
         if (a == ae || b == be) {
             st = 1;  // u or v isolated in G: unreachable, d = inf -> keep
+            cls = kWhyIsolated;
         } else {
             while (a < ae && b < be) {
                 int32_t x = gi[a], y = gi[b];
@@ -178,6 +208,7 @@ __global__ void k_bb_witness(const int64_t *__restrict__ src, const int64_t *__r
                     double path = gw[a] + gw[b];  // fl(fl(0 + w_ux) + w_xv)
                     if (wi > path + eps) {
                         st = 2;
+                        cls = kWhyWitness;
                         break;
                     }
                     w2 = path < w2 ? path : w2;
@@ -197,10 +228,14 @@ __global__ void k_bb_witness(const int64_t *__restrict__ src, const int64_t *__r
                 const double l3a = au + mv, l3b = mu + av, l3 = l3a > l3b ? l3a : l3b, l4 = au + av;
                 double lb = w2 < l3 ? w2 : l3;
                 lb = lb < l4 ? lb : l4;
-                if (wi <= lb * (1.0 - 2.0 * m)) st = 1;
+                if (wi <= lb * (1.0 - 2.0 * m)) {
+                    st = 1;
+                    cls = kWhyLocal34;
+                }
             }
         }
         state[i] = st;
+        if (why && st) why[i] = cls;
     }
 }
 
@@ -360,7 +395,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp(
     const double *__restrict__ w, double eps, uint8_t *__restrict__ state,
     unsigned long long *__restrict__ dist_all, int32_t *__restrict__ qflag_all,
     int32_t *__restrict__ fr_all, int32_t *__restrict__ touched_all, int64_t b0, int64_t b1,
-    int part, int nparts, unsigned long long *__restrict__ relax_total) {
+    int part, int nparts, unsigned long long *__restrict__ relax_total, uint8_t *__restrict__ why) {
     __shared__ int s_fcount, s_ncount, s_tcount;
     __shared__ double s_wmax, s_wnext;
     __shared__ unsigned long long s_relax;
@@ -408,7 +443,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp(
                 const unsigned long long db =
                     __hip_atomic_load(&dist[dst[idx]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (db != kInfBits && w[idx] > __longlong_as_double((long long)db) + eps) {
-                    state[idx] = 2;
+                    bb_set(state, why, idx, 2, kWhySearchPrune);
                     continue;
                 }
                 m = w[idx] > m ? w[idx] : m;
@@ -431,7 +466,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp(
                 __hip_atomic_load(&dist[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             double d = __longlong_as_double((long long)db);
             bool keep = (db == kInfBits) || (w[idx] <= d + eps);
-            state[idx] = keep ? 1 : 2;
+            bb_set(state, why, idx, keep ? 1 : 2, keep ? kWhySearchKeep : kWhySearchPrune);
         }
         __syncthreads();
         const int tc = s_tcount;
@@ -500,7 +535,7 @@ __device__ __forceinline__ bool bb_cross_decide(const uint64_t *__restrict__ ske
                                                 const int32_t *__restrict__ gi,
                                                 const double *__restrict__ gw,
                                                 const unsigned long long *__restrict__ dist,
-                                                uint8_t *__restrict__ state) {
+                                                uint8_t *__restrict__ state, uint8_t *__restrict__ why) {
     if (rp < 0) return false;
     const uint64_t rkey = (uint64_t)v * (uint64_t)n + (uint64_t)u;
     bool open = false;  // any reverse column still undecided
@@ -532,9 +567,9 @@ __device__ __forceinline__ bool bb_cross_decide(const uint64_t *__restrict__ ske
         const int64_t r = sidx[p];
         if (state[r] != 0) continue;
         const double wr = w[r];
-        if (exact) state[r] = wr <= D + eps ? 1 : 2;
-        else if (reached && wr > hi) state[r] = 2;
-        else if (keep_unreached && wr <= lo) state[r] = 1;
+        if (exact) bb_set(state, why, r, wr <= D + eps ? 1 : 2, kWhyRevExact);
+        else if (reached && wr > hi) bb_set(state, why, r, 2, kWhyRevPrune);
+        else if (keep_unreached && wr <= lo) bb_set(state, why, r, 1, kWhyRevKeep);
         else left = true;
     }
     // a v of more than kBbCrossDeg neighbours: the caller's workgroup scans them
@@ -628,8 +663,9 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
     const int64_t *__restrict__ sidx, const int64_t *__restrict__ rpos, int64_t E, double mrg,
     int rev, int64_t b0, int64_t b1, int part, int nparts,
     unsigned long long *__restrict__ batch_next, unsigned long long *__restrict__ relax_total,
-    unsigned long long *__restrict__ trace, const uint8_t *__restrict__ lmflag = nullptr,
-    const double *__restrict__ LD = nullptr, const int32_t *__restrict__ lcomp = nullptr, int K = 0) {
+    unsigned long long *__restrict__ trace, uint8_t *__restrict__ why,
+    const uint8_t *__restrict__ lmflag = nullptr, const double *__restrict__ LD = nullptr,
+    const int32_t *__restrict__ lcomp = nullptr, int K = 0) {
     static_assert(S >= 1 && S <= 16, "1..16 sources per workgroup");
     static_assert(!PAIR || S == 2, "the pair form searches both ends of one column");
     // queue bits of the per-node mask; the near-far order needs S more bits for the
@@ -1020,7 +1056,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                                 &dist[dst[idx] * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             if (db != kInfBits &&
                                 w[idx] > __longlong_as_double((long long)db) + eps) {
-                                state[idx] = 2;
+                                bb_set(state, why, idx, 2, kWhySearchPrune);
                                 continue;
                             }
                             const unsigned long long kk = dkey(w[idx]);
@@ -1179,9 +1215,9 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                     if (state[c] != 0) return;
                     const double wc = w[c];
                     if (!(wc <= 2.0 * r * (1.0 - 5.0 * mrg))) return;
-                    if (has && wc > wg + eps) state[c] = 2;
-                    else if (M * (1.0 - 5.0 * mrg) >= wc) state[c] = 1;
-                    else if ((M * (1.0 + 4.0 * mrg) + eps) * (1.0 + mrg) < wc) state[c] = 2;
+                    if (has && wc > wg + eps) bb_set(state, why, c, 2, kWhyMitm);
+                    else if (M * (1.0 - 5.0 * mrg) >= wc) bb_set(state, why, c, 1, kWhyMitm);
+                    else if ((M * (1.0 + 4.0 * mrg) + eps) * (1.0 + mrg) < wc) bb_set(state, why, c, 2, kWhyMitm);
                 };
                 decide(s_pcol);
                 const int64_t rp = rpos[s_pcol];
@@ -1207,10 +1243,13 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                 const unsigned long long db = __hip_atomic_load(
                     &dist[v * S + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const double d = __longlong_as_double((long long)db);
-                if (st0 == 0) state[idx] = ((db == kInfBits) || (w[idx] <= d + eps)) ? 1 : 2;
+                if (st0 == 0) {
+                    const bool keep = (db == kInfBits) || (w[idx] <= d + eps);
+                    bb_set(state, why, idx, keep ? 1 : 2, keep ? kWhySearchKeep : kWhySearchPrune);
+                }
                 if (cross &&
                     bb_cross_decide<S>(skeys, sidx, rpos[idx], u, v, n, E, k, db, bk, mrg, eps, w, gp, gi,
-                                       gw, dist, state)) {
+                                       gw, dist, state, why)) {
                     const int q = atomicAdd(&s_nbig, 1);
                     if (q < kBbCrossBig) s_big[q] = (idx << 4) | k;
                 }
@@ -1251,7 +1290,7 @@ __global__ void __launch_bounds__(NT) k_bb_sssp_multi(
                         const uint64_t rkey = (uint64_t)v * (uint64_t)n + (uint64_t)u;
                         for (int64_t p = rpos[idx]; p < E && skeys[p] == rkey; ++p) {
                             const int64_t r = sidx[p];
-                            if (state[r] == 0) state[r] = w[r] <= D + eps ? 1 : 2;
+                            if (state[r] == 0) bb_set(state, why, r, w[r] <= D + eps ? 1 : 2, kWhyRevExact);
                         }
                     }
                     s_amin = kInfBits;
@@ -1649,7 +1688,8 @@ __global__ void k_bb_certify(const int64_t *__restrict__ src, const int64_t *__r
                              const double *__restrict__ gw, const double *__restrict__ D,
                              const int32_t *__restrict__ complete, int K, double eps, double m,
                              const double *__restrict__ mw, const int32_t *__restrict__ ma,
-                             int part, int nparts, uint8_t *__restrict__ state) {
+                             int part, int nparts, uint8_t *__restrict__ state,
+                             uint8_t *__restrict__ why) {
     for (int64_t i = c0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < c1;
          i += (int64_t)gridDim.x * blockDim.x) {
         if (state[i] != 0) continue;  // decided, or another part's column (3)
@@ -1660,7 +1700,7 @@ __global__ void k_bb_certify(const int64_t *__restrict__ src, const int64_t *__r
         const int64_t du = gp[u + 1] - gp[u], dv = gp[v + 1] - gp[v];
         if ((du == 1 && gi[gp[u]] == v) || (dv == 1 && gi[gp[v]] == u)) {
             const double wg = du == 1 && gi[gp[u]] == v ? gw[gp[u]] : gw[gp[v]];
-            state[i] = (wi <= wg + eps) ? 1 : 2;  // d = fl(0 + w_G) = w_G
+            bb_set(state, why, i, (wi <= wg + eps) ? 1 : 2, kWhyDeg1);  // d = fl(0 + w_G) = w_G
             continue;
         }
         if (mw) {
@@ -1679,33 +1719,41 @@ __global__ void k_bb_certify(const int64_t *__restrict__ src, const int64_t *__r
             const double mv = ma[v] == (int32_t)u ? mw[2 * v + 1] : mw[2 * v];
             const double lb = (mu + mv) * (1.0 - 2.0 * m);  // +inf when either is missing
             if (has && wi > gw[lo] + eps) {
-                state[i] = 2;
+                bb_set(state, why, i, 2, kWhyDirect);
                 continue;
             }
             if (wi <= lb) {
-                state[i] = 1;
+                bb_set(state, why, i, 1, kWhyLocal2);
                 continue;
             }
         }
-        uint8_t st = 0;
+        uint8_t st = 0, cls = kWhyOpen;
         for (int l = 0; l < K && !st; ++l) {
             const double a = D[u * K + l], b = D[v * K + l];
             const bool fa = a != __builtin_inf(), fb = b != __builtin_inf();
             const bool exact = complete[l] != 0;  // else D holds upper bounds only
             if (fa != fb) {
-                if (exact) st = 1;  // different components
+                if (exact) {
+                    st = 1;  // different components
+                    cls = kWhyLmComp;
+                }
             } else if (fa) {
                 const double ub = (a + b) * (1.0 + m);
                 if (wi > ub + eps) {
                     st = 2;
+                    cls = kWhyLmPrune;
                 } else if (exact) {
                     const double hi = a > b ? a : b, lo = a > b ? b : a;
                     const double lb = (hi - lo) - m * (hi + lo);
-                    if (wi <= lb) st = 1;
+                    if (wi <= lb) {
+                        st = 1;
+                        cls = kWhyLmKeep;
+                    }
                 }
             }
         }
         state[i] = st;
+        if (why && st) why[i] = cls;
     }
 }
 
@@ -1895,6 +1943,10 @@ struct BbRun {
     double wmed = 0.0;
     int64_t *optr = nullptr, *order = nullptr;
     uint8_t *state = nullptr;
+    // decision classes (gs_bb_classes): why[E] written beside state when why_on
+    bool why_on = false;
+    uint8_t *why = nullptr;
+    int64_t why_E = 0;
     int K = 0;
     double *D = nullptr;
     int32_t *lcomp = nullptr;
@@ -2011,6 +2063,13 @@ static void bb_begin(gs_ctx *c, int64_t n, int64_t E, const int64_t *src, const 
     GS_HIP(hipMemsetAsync(R.misc, 0, 64, s));
     R.state = (uint8_t *)b_state.ensure(E ? E : 1);
     if (E) GS_HIP(hipMemsetAsync(R.state, 0, E, s));
+    R.why = nullptr;
+    R.why_E = 0;
+    if (R.why_on) {
+        R.why = (uint8_t *)c->buf("bb_why").ensure(E ? E : 1);
+        if (E) GS_HIP(hipMemsetAsync(R.why, 0, E, s));
+        R.why_E = E;
+    }
     R.tall = prof_begin(c);
     if (E > 0) {
         hipEvent_t t0 = prof_begin(c);  // ended as "bb_build" below (no leak at E = 0)
@@ -2193,11 +2252,11 @@ static void bb_certify(gs_ctx *c, int part, int nparts) {
             k_bb_certify<<<grid_for(c1 - c0, 256, 8192), 256, 0, s>>>(R.dsrc, R.ddst, R.dw, c0, c1, R.gp,
                                                                        R.gi, R.gw, R.D, R.lcomp, R.K,
                                                                        R.eps, mrg, mw, ma, R.pair_part,
-                                                                       R.pair_nparts, R.state);
+                                                                       R.pair_nparts, R.state, R.why);
         }
         k_bb_witness<<<grid_for(c1 - c0, 256, 8192), 256, 0, s>>>(
             R.dsrc, R.ddst, R.dw, c0, c1, R.gp, R.gi, R.gw, R.eps, R.pair_part, R.pair_nparts, mw, ma,
-            aw, aa, mrg, R.state);
+            aw, aa, mrg, R.state, R.why);
         // the meet-in-the-middle certificate of the columns still open (k_bb_sssp_multi
         // PAIR: both ends searched to half the column's weight; GSPARSE_BB_MITM=1: on).
         // It needs the local bounds' direct-edge rule, so it runs only with them.  Off by
@@ -2273,7 +2332,7 @@ static void bb_certify(gs_ctx *c, int part, int nparts) {
                 k_bb_sssp_multi<512, 2, true><<<(unsigned)P, 512, 0, s>>>(
                     R.gp, R.gi, R.gw, R.n, plist, np, R.optr, R.order, R.dsrc, R.ddst, R.dw, R.eps, R.state,
                     dist, qm, fr, fm, tch, farl, delta, 0, R.skeys, R.sidx, R.rpos, R.E, mrg, 0, 0, np, 0, 1,
-                    bnext, R.misc + 1, trace, lmf, R.D, R.lcomp, R.K);
+                    bnext, R.misc + 1, trace, R.why, lmf, R.D, R.lcomp, R.K);
                 GS_HIP(hipGetLastError());
                 if (tpath) {
                     std::vector<unsigned long long> h(6 * (size_t)np);
@@ -2440,7 +2499,7 @@ static void bb_search(gs_ctx *c, int64_t b0, int64_t b1, int part, int nparts) {
         auto kfn = R.bt == 1024 ? k_bb_sssp<1024> : R.bt == 512 ? k_bb_sssp<512> : k_bb_sssp<256>;
         kfn<<<grid, R.bt, 0, s>>>(R.gp, R.gi, R.gw, R.n, R.sources, R.nsrc, R.optr, R.order, R.ddst,
                                   R.dw, R.eps, R.state, R.dist, R.qflag, R.fr, R.touched, b0, b1, part,
-                                  nparts, R.misc + 1);
+                                  nparts, R.misc + 1, R.why);
     } else {
         unsigned long long *bnext = R.dynamic ? R.misc + 2 : nullptr;
         if (bnext) GS_HIP(hipMemsetAsync(bnext, 0, 8, s));
@@ -2460,7 +2519,7 @@ static void bb_search(gs_ctx *c, int64_t b0, int64_t b1, int part, int nparts) {
                                                    qm, R.fr, R.fm, R.touched, R.farl, R.delta,     \
                                                    R.cross, R.skeys, R.sidx, R.rpos, R.E, mrg,     \
                                                    R.rev, b0, b1, part, nparts, bnext, R.misc + 1, \
-                                                   trace)
+                                                   trace, R.why)
         const int S = R.S;
         if (R.bt == 1024) {
             if (S == 2) GS_BBM(1024, 2); else if (S == 4) GS_BBM(1024, 4);
@@ -2617,6 +2676,54 @@ extern "C" int gs_bb_finish(gs_ctx *c, uint8_t *keep, int keep_loc, int64_t *n_r
     return guard([&] {
         GS_CHECK(c, GS_EINVAL, "null context");
         bb_finish(c, keep, keep_loc, n_relax);
+    });
+}
+
+__global__ void k_bb_why_hist(const uint8_t *__restrict__ why, int64_t E,
+                              unsigned long long *__restrict__ cnt) {
+    __shared__ unsigned int h[kWhyClasses];
+    for (int k = threadIdx.x; k < kWhyClasses; k += blockDim.x) h[k] = 0;
+    __syncthreads();
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint8_t k = why[i];
+        atomicAdd(&h[k < kWhyClasses ? k : 0], 1u);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kWhyClasses; k += blockDim.x)
+        if (h[k]) atomicAdd(&cnt[k], (unsigned long long)h[k]);
+}
+
+extern "C" int gs_bb_classes(gs_ctx *c, int on) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        bb_run(c).why_on = on != 0;
+    });
+}
+
+extern "C" int gs_bb_class_counts(gs_ctx *c, int64_t *counts, int ncounts, uint8_t *why, int64_t nwhy,
+                                  int why_loc, int64_t *n_columns) {
+    return guard([&] {
+        GS_CHECK(c, GS_EINVAL, "null context");
+        GS_CHECK(counts && ncounts >= (int)kWhyClasses, GS_EINVAL, "counts needs %d entries", (int)kWhyClasses);
+        BbRun &R = bb_run(c);
+        GS_CHECK(R.why_on && R.why, GS_ESTATE, "gs_bb_classes(ctx, 1) before the backbone run");
+        GS_CHECK(!why || nwhy >= R.why_E, GS_EINDEX, "why holds %lld bytes, the run has %lld columns",
+                 (long long)nwhy, (long long)R.why_E);
+        if (n_columns) *n_columns = R.why_E;
+        GS_HIP(hipSetDevice(c->device));
+        hipStream_t s = c->stream;
+        auto *d = (unsigned long long *)c->buf("bb_whycnt").ensure(8 * kWhyClasses);
+        GS_HIP(hipMemsetAsync(d, 0, 8 * kWhyClasses, s));
+        if (R.why_E > 0) k_bb_why_hist<<<grid_for(R.why_E, 256, 2048), 256, 0, s>>>(R.why, R.why_E, d);
+        GS_HIP(hipGetLastError());
+        unsigned long long h[kWhyClasses];
+        GS_HIP(hipMemcpyAsync(h, d, 8 * kWhyClasses, hipMemcpyDeviceToHost, s));
+        if (why && R.why_E > 0)
+            GS_HIP(hipMemcpyAsync(why, R.why, R.why_E,
+                                  why_loc == GS_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+        GS_HIP(hipStreamSynchronize(s));
+        for (int k = 0; k < ncounts; ++k) counts[k] = k < (int)kWhyClasses ? (int64_t)h[k] : 0;
     });
 }
 

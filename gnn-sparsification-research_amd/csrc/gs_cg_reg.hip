@@ -138,8 +138,10 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     // sums / tail rows, the chunk table
     const int nch = 32 * T;
     const bool ufast = unit && dcount;  // the unit kernels derive every diagonal from the entry count
-    // (512 threads, two per chain, unit: the diagonal slots bank-permuted, k_cg_regwide DBANK)
-    const bool dbank = NT == 512 && G == 2 && ufast;
+    // (512 threads, two per chain, unit: the diagonal slots bank-permuted -- the same
+    // condition as k_cg_regwide's DBANK = GS_CG_V2 && UNIT && G == 2, so an A/B build with
+    // -DGS_CG_V2=0 codes the diagonal where its kernel reads it)
+    const bool dbank = GS_CG_V2 && NT == 512 && G == 2 && ufast;
     const int dsl = NT == 256 ? 2 * NT : ufast ? NT : 0;
     const size_t lds_max = 160 * 1024;
     const int64_t cap =
@@ -179,7 +181,7 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     double regv = c->er.reg;
     int64_t regbits;
     memcpy(&regbits, &regv, sizeof(regbits));
-    std::vector<int64_t> key = {c->g.epoch, regbits, n, T, G, NT, ufast ? 1 : 0, unit, dcount};
+    std::vector<int64_t> key = {c->g.epoch, regbits, n, T, G, NT, ufast ? 1 : 0, unit, dcount, dbank ? 1 : 0};
     for (int t = 0; t < T; ++t) key.insert(key.end(), {ha[t], hlen[t], keep[t]});
     auto *ocnt = (int64_t *)c->buf("er_reg_ocnt").ensure(sizeof(int64_t) * (n + 1));
     auto *optr = (int64_t *)c->buf("er_reg_optr").ensure(sizeof(int64_t) * (n + 1));

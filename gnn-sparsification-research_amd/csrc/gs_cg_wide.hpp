@@ -9,6 +9,17 @@
 #pragma once
 #include "gs_cg_reg.hpp"
 
+// -DGS_CG_QS=1: whole columns (x in registers) store q = L_reg p of the SpMV pass in the
+// column's own Xc output column (L2 / Infinity Cache scratch until x is written there at
+// the end), and the r update reads it back (GS_CG_QPRE slots ahead) instead of
+// recomputing the SpMV: one SpMV per iteration, the same arithmetic
+#ifndef GS_CG_QS
+#define GS_CG_QS 0
+#endif
+#ifndef GS_CG_QPRE
+#define GS_CG_QPRE 4
+#endif
+
 namespace gs {
 
 // byte address (p code * 8) of the low / high 16-bit p code of an ELL word: one SDWA
@@ -70,6 +81,8 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     // V2, two threads per chain: each lane's diagonal slot in the bank after its own p
     // rows' bank (see dslot below)
     constexpr bool DBANK = V2 && G == 2;
+    // q of the SpMV pass kept for the r update in the column's Xc column (GS_CG_QS)
+    constexpr bool QS = GS_CG_QS && !QR && !SPLIT;
     extern __shared__ double lds[];
     const int part = SPLIT ? (int)(blockIdx.x % (unsigned)A.P) : 0;
     const int group = SPLIT ? (int)(blockIdx.x / (unsigned)A.P) : (int)blockIdx.x;
@@ -524,6 +537,18 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             __builtin_amdgcn_raw_buffer_store_b64(
                 __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), xrs, base * 8, 256 * G * u, 0);
         };
+        // QS: q of slot u to / from the Xc column (rows of slots past the lane's chain rows
+        // are not this lane's: their offset lies past the buffer, so the store is dropped
+        // and the load reads 0.0)
+        auto qstore = [&](int u, double v) {
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), xrs,
+                valid(u) ? base * 8 : kOob, 256 * G * u, 0);
+        };
+        auto qload = [&](int u) -> double {
+            return __builtin_bit_cast(
+                double, __builtin_amdgcn_raw_buffer_load_b64(xrs, valid(u) ? base * 8 : kOob, 256 * G * u, 0));
+        };
         // r = b.copy(); rho_0 = b.b
         {
             launder();
@@ -717,6 +742,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                         if (valid(u)) qv = spmv2(rowof(u), eb[u], db[u], pv, u);
                     } else if (valid(u)) qv = spmv(rowof(u), eb[u], lb[u], pv, u);
                     if constexpr (QR) qr[u] = qv;
+                    if constexpr (QS) qstore(u, qv);
                     chain_step(acc, pv, qv, u);
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -758,6 +784,29 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                 if (tail) {
                     const double t1 = alpha * side_p[tix];
                     side_x[tix] = side_x[tix] + t1;
+                    const double t2 = alpha * side_q[tix];
+                    side_r[tix] = side_r[tix] - t2;
+                }
+            } else if constexpr (QS) {
+                // r -= alpha q (q from the SpMV pass, read back from the Xc column), chains of r.r
+                launder();
+                double acc = 0.0;
+                constexpr int kPq = GS_CG_QPRE;
+                double qb[R];
+#pragma unroll
+                for (int u = 0; u < kPq && u < R; ++u) qb[u] = qload(u);
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    if (u + kPq < R) qb[u + kPq] = qload(u + kPq);
+                    if (valid(u)) {
+                        const double t2 = alpha * qb[u];
+                        r[u] = r[u] - t2;
+                    }
+                    chain_step(acc, r[u], r[u], u, true);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (g == 0 && live) acc_rr[chain] = acc;
+                if (tail) {
                     const double t2 = alpha * side_q[tix];
                     side_r[tix] = side_r[tix] - t2;
                 }

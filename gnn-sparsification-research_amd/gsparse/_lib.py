@@ -80,6 +80,15 @@ SIGNATURES = {
     "gs_bb_plan": (_int, [_vp, ctypes.POINTER(_i64)]),
     "gs_bb_search": (_int, [_vp, _i64, _i64, _int, _int]),
     "gs_bb_finish": (_int, [_vp, _vp, _int, ctypes.POINTER(_i64)]),
+    "gs_bb_classes": (_int, [_vp, _int]),
+    "gs_jsel_begin": (_int, [_vp, _int, _int, _vp, _int, _i64, _int, _vp, _vp, _int]),
+    "gs_jsel_step": (_int, [_vp, _vp, ctypes.POINTER(_int)]),
+    "gs_jsel_result": (_int, [_vp, ctypes.POINTER(_f64), ctypes.POINTER(_i64), ctypes.POINTER(_i64),
+                              ctypes.POINTER(_i64)]),
+    "gs_jsel_tie_positions": (_int, [_vp, _vp, _i64, _int]),
+    "gs_jsel_keep": (_int, [_vp, _vp, _i64, _int, _i64, _vp, _int]),
+    "gs_jsel_mask": (_int, [_vp, _int, _vp, _i64, _int, _vp, _int]),
+    "gs_bb_class_counts": (_int, [_vp, _vp, _int, _vp, _i64, _int, ctypes.POINTER(_i64)]),
     "gs_exact_er": (_int, [_vp, _vp, _int, ctypes.POINTER(_i32)]),
     "gs_pair_distances": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _i64, _int, _i64, _vp, _vp,
                                  _vp]),

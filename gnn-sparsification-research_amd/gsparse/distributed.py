@@ -21,6 +21,9 @@ SURVEY §8(e):
   * the global top-k (sharded_sparsify): every rank holds the all-gathered
     scores and runs the same radix select on its own device -- the kept set is
     identical on every rank and to one GPU's, with no further exchange.
+  * Jaccard-T without the score exchange (sharded_jaccard_topk): the ranks radix-select
+    the cut over their own owner pairs with all-reduced histograms (gs_jsel_*), then
+    all-gather one keep byte per pair -- no replicated score scatter or full top-k.
   * ApproxER: the k JL columns are independent CG solves.  Rank blocks are
     nodes of NumPy's pairwise-sum tree over k (gs_er_split), so each rank's
     per-edge partial sum is exactly a subtree of the reference's
@@ -240,6 +243,101 @@ def sharded_sparsify(engine, comm: Comm, scores, num_edges: int, retention_ratio
     return mask.view(torch.bool) if mask.dtype == torch.uint8 else mask, info
 
 
+def _engine_device(engine) -> torch.device:
+    ctx = getattr(engine, "ctx", None)
+    return torch.device("cuda", ctx.device) if ctx is not None else torch.device("cpu")
+
+
+def sharded_jaccard_topk(engine, comm: Comm, retention_ratio: float, keep_lowest: bool = False,
+                         tie_break: str | None = None, mask_out=None, scores_out=None):
+    """Jaccard-T over ranks (metrics.py:17-64 scores, then core.py:229-240's global top-k)
+    without gathering the scores: every rank counts its owner pairs
+    (gs_jaccard_part_counts), scores and keys them, and the ranks select the cut together
+    by radix select over all-reduced histograms (gs_jsel_*: five passes, one SUM
+    all-reduce of <= 64 KB each); an ambiguous tie block exchanges only its positions;
+    each rank then sends one keep byte per own pair (an all-gather of ~E / 2 bytes in
+    all) and every rank writes the whole CSR keep mask.
+
+    The kept set equals a single GPU's ``sparsify`` on the same scores: the device tie
+    rule (np.argsort(kind='stable')) for tie_break="stable"; for "numpy" (the default,
+    $GSPARSE_TIE_BREAK) an ambiguous cut is resolved by the reference's own np.argsort on
+    the gathered scores -- the only case that gathers them.  E = nnz (a symmetric graph's
+    CSR entries; the bench's R-MAT).
+
+    Returns (mask, info, scores): mask a uint8 tensor of nnz on the engine's device (or
+    ``mask_out``), info the cut / #beyond / #tied / need / ambiguous, scores this rank's
+    owner-pair scores (``scores_out`` if given; owner order of its row share)."""
+    import os
+
+    if not 0 < retention_ratio <= 1:
+        raise ValueError(f"retention_ratio must be in (0, 1], got {retention_ratio}")
+    tie_break = tie_break or os.environ.get("GSPARSE_TIE_BREAK", "numpy")
+    if tie_break not in ("numpy", "stable"):
+        raise ValueError(f"tie_break must be 'numpy' or 'stable', got {tie_break!r}")
+    nnz = engine.nnz
+    dev = _engine_device(engine)
+    _, oo = engine.jaccard_shares(comm.world)
+    sizes = np.diff(oo)
+    stride = max(1, int(sizes.max()) if len(sizes) else 1)
+    mine_pairs = int(sizes[comm.rank])
+    counts = torch.zeros(stride, dtype=torch.int32, device=dev)
+    if dev.type == "cuda":
+        engine.jaccard_part_counts(comm.rank, comm.world, out=counts)
+    else:
+        part = np.asarray(engine.jaccard_part_counts(comm.rank, comm.world), dtype=np.uint32)
+        counts[: part.shape[0]] = torch.from_numpy(part.view(np.int32))
+    mask = mask_out if mask_out is not None else torch.empty(max(nnz, 1), dtype=torch.uint8, device=dev)
+    num_keep = int(nnz * retention_ratio)
+    if scores_out is None:
+        scores_out = torch.empty(max(mine_pairs, 1), dtype=torch.float64, device=dev)
+    if num_keep <= 0 or num_keep >= nnz:
+        # nothing to select: idx[-0:] keeps all (top), idx[:0] none (keep_lowest)
+        kept = not (keep_lowest and num_keep <= 0)
+        mask[:nnz].fill_(1 if kept else 0)
+        info = {"cut": None, "beyond": nnz if kept else 0, "tied": 0, "need": 0, "ambiguous": False}
+        return mask, info, None
+
+    def all_reduce(t):
+        if t.device == comm.device:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=comm.group)
+        else:
+            c = t.to(comm.device)
+            dist.all_reduce(c, op=dist.ReduceOp.SUM, group=comm.group)
+            t.copy_(c)
+
+    hist = torch.zeros(engine.JSEL_BINS, dtype=torch.int64, device=dev)
+    engine.jsel_begin(comm.rank, comm.world, counts, num_keep, keep_lowest, hist, scores_out)
+    left = engine.JSEL_PASSES
+    while left:
+        all_reduce(hist)
+        left = engine.jsel_step(hist)
+    cut, nb, nt, my_tied = engine.jsel_result()
+    need = num_keep - nb
+    info = {"cut": cut, "beyond": nb, "tied": nt, "need": need, "ambiguous": 0 < need < nt}
+    if info["ambiguous"] and tie_break == "numpy":
+        from .selection import numpy_topk_mask
+
+        s = sharded_jaccard(engine, comm)
+        s = s.cpu().numpy() if isinstance(s, torch.Tensor) else np.asarray(s)
+        m = torch.from_numpy(numpy_topk_mask(s, nnz, num_keep, keep_lowest).astype(np.uint8))
+        mask[:nnz].copy_(m.to(mask.device))
+        return mask, info, scores_out
+    tie_all = None
+    if info["ambiguous"]:
+        cnt = comm.all_gather_same(torch.tensor([my_tied], dtype=torch.int64))
+        tsz = [int(x.item()) for x in cnt]
+        pos = torch.zeros(max(1, my_tied), dtype=torch.int64, device=dev)
+        engine.jsel_tie_positions(pos)
+        tie_all = comm.all_gather_padded(pos[:my_tied], tsz).to(dev)
+        if tie_all.numel() != nt:
+            raise RuntimeError(f"tie block: {tie_all.numel()} positions gathered, {nt} expected")
+    keep = torch.zeros(stride, dtype=torch.uint8, device=dev)
+    engine.jsel_keep(tie_all, nt, need, keep)
+    kall = comm.all_gather_flat(keep).to(dev)
+    engine.jsel_mask(comm.world, kall, stride, mask)
+    return mask, info, scores_out
+
+
 def backbone_phases(nbatch: int, world: int, fractions=None) -> list[tuple[int, int]]:
     """Search ranges of the staged backbone: batches [b0, b1) of the ascending-count
     order, cut at the given fractions of nbatch (default $GSPARSE_BB_PHASES, else
@@ -307,11 +405,30 @@ def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
     if method != "staged":
         raise ValueError(f"method must be 'staged' or 'pairs', got {method!r}")
     K = st.begin(edge_index, num_nodes, edge_weights, epsilon, comm.rank, comm.world)
-    if K and comm.world > 1:
-        D = torch.empty(K * num_nodes, dtype=torch.float64, device=comm.device)
+    if comm.world > 1:
+        # every rank must run the same schedule (the same number of collectives), whatever
+        # its own environment says: K and the search ranges are checked / taken from rank 0
+        agree = torch.tensor([K, -K], dtype=torch.int64, device=comm.device)
+        dist.all_reduce(agree, op=dist.ReduceOp.MAX, group=comm.group)
+        if int(agree[0]) != K or int(-agree[1]) != K:
+            raise RuntimeError(f"ranks disagree on the landmark count (this rank {K}, range "
+                               f"[{int(-agree[1])}, {int(agree[0])}]): set GSPARSE_BB_LANDMARKS alike")
+    if K and comm.world > 1 and E and num_nodes:
+        # rank r searched landmarks l = r (mod N) and holds only their labels (D is node-major,
+        # D[u K + l]): each rank sends its own columns, every rank rebuilds the table
+        n_ = int(num_nodes)
+        D = torch.empty(K * n_, dtype=torch.float64, device=comm.device)
         comp = torch.empty(K, dtype=torch.int32, device=comm.device)
         st.landmarks_io(D, comp, out=True)
-        dist.all_reduce(D, op=dist.ReduceOp.MIN, group=comm.group)
+        per = (K + comm.world - 1) // comm.world
+        mine = torch.arange(comm.rank, K, comm.world, device=comm.device)
+        send = torch.full((n_, per), float("inf"), dtype=torch.float64, device=comm.device)
+        send[:, : mine.numel()] = D.view(n_, K)[:, mine]
+        got = comm.all_gather_flat(send.reshape(-1)).view(comm.world, n_, per)
+        Dv = D.view(n_, K)
+        for r in range(comm.world):
+            cols = torch.arange(r, K, comm.world, device=comm.device)
+            Dv[:, cols] = got[r, :, : cols.numel()]
         dist.all_reduce(comp, op=dist.ReduceOp.MAX, group=comm.group)
         st.landmarks_io(D, comp, out=False)
     st.certify(comm.rank, comm.world)
@@ -325,7 +442,19 @@ def sharded_backbone(comm: Comm, edge_index, num_nodes: int, edge_weights,
 
     exchange()
     nb = st.plan()
-    for b0, b1 in backbone_phases(nb, comm.world, phases):
+    ranges = backbone_phases(nb, comm.world, phases)
+    if comm.world > 1:  # rank 0's ranges ($GSPARSE_BB_PHASES / `phases` may differ per rank)
+        cuts = torch.zeros(66, dtype=torch.int64, device=comm.device)
+        if comm.rank == 0:
+            if len(ranges) > 64:
+                raise ValueError(f"at most 64 search ranges, got {len(ranges)}")
+            cuts[0] = len(ranges)
+            cuts[1: len(ranges) + 2] = torch.tensor([b for b, _ in ranges] + [nb], dtype=torch.int64)
+        comm.broadcast_from(cuts, 0)
+        k = int(cuts[0])
+        b = [int(x) for x in cuts[1: k + 2]]
+        ranges = list(zip(b[:-1], b[1:]))
+    for b0, b1 in ranges:
         st.search(b0, b1, comm.rank, comm.world)
         exchange()
     keep = keep_out if keep_out is not None else torch.empty(max(E, 1), dtype=torch.uint8,

@@ -141,6 +141,88 @@ class Engine:
         self.ctx.call("gs_jaccard_from_counts", nparts, ptr(counts), stride, cloc, ptr(o), loc)
         return o
 
+    # -- distributed Jaccard-T select (gs_jsel_*, include/gsparse.h) ---------
+    JSEL_BINS, JSEL_PASSES = 8192, 5
+
+    @staticmethod
+    def _loc(a):
+        if isinstance(a, np.ndarray):
+            return GS_HOST
+        return GS_DEVICE if a.is_cuda else GS_HOST
+
+    @staticmethod
+    def _need(a, count, dtypes, what):
+        n = a.size if isinstance(a, np.ndarray) else a.numel()
+        dt = a.dtype if isinstance(a, np.ndarray) else a.dtype
+        if dt not in dtypes:
+            raise TypeError(f"{what} must be one of {dtypes}, got {dt}")
+        if n < count:
+            raise IndexError(f"{what} holds {n} < {count} values")
+
+    def jsel_begin(self, part: int, nparts: int, counts, num_keep: int, keep_lowest: bool, hist,
+                   scores=None):
+        """Keys (and, into ``scores``, the fp64 scores) of this part's owner pairs and the
+        first weighted histogram into ``hist`` (JSEL_BINS int64/uint64 values)."""
+        import torch
+
+        _, oo = self.jaccard_shares(nparts)
+        np_ = int(oo[part + 1] - oo[part])
+        self._need(counts, np_, (np.uint32, np.int32, torch.int32), "counts")
+        self._need(hist, self.JSEL_BINS, (np.uint64, np.int64, torch.int64), "hist")
+        if self._loc(hist) != GS_DEVICE:
+            raise ValueError("hist must be a device tensor (the ranks all-reduce it there)")
+        sloc = GS_HOST
+        if scores is not None:
+            self._need(scores, np_, (np.float64, torch.float64), "scores")
+            sloc = self._loc(scores)
+        self.ctx.call("gs_jsel_begin", int(part), int(nparts), ptr(counts), self._loc(counts),
+                      int(num_keep), int(bool(keep_lowest)), ptr(hist), ptr(scores), sloc)
+        return np_
+
+    def jsel_step(self, hist) -> int:
+        """One pass of the select on the all-reduced ``hist``; returns the passes left."""
+        left = ctypes.c_int(0)
+        self.ctx.call("gs_jsel_step", ptr(hist), ctypes.byref(left))
+        return left.value
+
+    def jsel_result(self):
+        """(cut, #beyond, #tied, #tied positions on this rank)."""
+        cut, nb, nt, mine = ctypes.c_double(0), ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        self.ctx.call("gs_jsel_result", ctypes.byref(cut), ctypes.byref(nb), ctypes.byref(nt),
+                      ctypes.byref(mine))
+        return cut.value, nb.value, nt.value, mine.value
+
+    def jsel_tie_positions(self, out):
+        """This rank's tied CSR positions into ``out`` (int64)."""
+        import torch
+
+        self._need(out, 0, (np.int64, torch.int64), "positions")
+        n = out.size if isinstance(out, np.ndarray) else out.numel()
+        self.ctx.call("gs_jsel_tie_positions", ptr(out), int(n), self._loc(out))
+        return out
+
+    def jsel_keep(self, tie_pos, ntie: int, need: int, out):
+        """Keep bytes of this part's pairs (bit 0 owner entry, bit 1 reverse entry)."""
+        import torch
+
+        self._need(out, 0, (np.uint8, torch.uint8), "keep")
+        tloc = GS_HOST
+        if tie_pos is not None:
+            self._need(tie_pos, ntie, (np.int64, torch.int64), "tie positions")
+            tloc = self._loc(tie_pos)
+        self.ctx.call("gs_jsel_keep", ptr(tie_pos), int(ntie), tloc, int(need), ptr(out), self._loc(out))
+        return out
+
+    def jsel_mask(self, nparts: int, keep_all, stride: int, out):
+        """Every part's keep bytes (part p at p * stride) -> the CSR keep mask (uint8)."""
+        import torch
+
+        self._need(keep_all, nparts * stride, (np.uint8, torch.uint8), "keep_all")
+        self._need(out, self.nnz, (np.uint8, torch.uint8, torch.bool), "mask")
+        self.ctx.call("gs_jsel_mask", int(nparts), ptr(keep_all), int(stride), self._loc(keep_all),
+                      ptr(out), self._loc(out))
+        return out
+
     def adamic_adar(self, e0: int = 0, e1: int | None = None, out=None, c=None):
         e1 = self.nnz if e1 is None else e1
         if c is None:

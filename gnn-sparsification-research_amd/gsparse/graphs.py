@@ -129,6 +129,9 @@ def citation_like(n: int = 169_343, m: int = 1_166_243, seed: int = 0) -> np.nda
     (m / (n - 1) = 6.89): every node cites floor(m / (n-1)), a seeded choice of
     the others one more; citations lost to duplicates are topped up by fresh
     draws (uniform citing node, same target rule) until exactly m remain."""
+    if n < 2 or m < 0 or m > n * (n - 1) // 2:
+        raise ValueError(f"citation_like: {m} distinct citations need 0 <= m <= n (n - 1) / 2 "
+                         f"= {max(0, n * (n - 1) // 2)} (n = {n})")
     rng = np.random.default_rng(seed)
     nodes = np.arange(1, n, dtype=np.int64)
     base, extra = divmod(m, n - 1)
@@ -143,7 +146,13 @@ def citation_like(n: int = 169_343, m: int = 1_166_243, seed: int = 0) -> np.nda
         return np.minimum(np.where(copy, d[j], d), s - 1)
 
     keys = np.unique(src * n + targets(src))
+    rounds = 0
     while keys.size < m:
+        # near the n (n - 1) / 2 limit fresh pairs get rare: bounded rounds, then a loud stop
+        rounds += 1
+        if rounds > 10_000:
+            raise RuntimeError(f"citation_like: {keys.size} of {m} distinct citations after "
+                               f"{rounds - 1} top-up rounds (m is too close to n (n - 1) / 2)")
         need = m - keys.size
         s = rng.integers(1, n, size=2 * need + 1024, dtype=np.int64)
         k = s * n + targets(s)

@@ -70,7 +70,13 @@ def backbone_mask(edge_index: np.ndarray, num_nodes: int, edge_weights: np.ndarr
 class BackboneStages:
     """The staged prune on one context (gs_bb_*, include/gsparse.h): what one rank of
     ``gsparse.distributed.sharded_backbone`` runs between its exchanges.  Array
-    arguments are NumPy arrays / CPU tensors (host) or device tensors."""
+    arguments are NumPy arrays / CPU tensors (host) or device tensors.
+
+    The library reads 8 B per column of src / dst / weights and writes 1 B per column
+    of keep / state, so every buffer is checked here before its pointer is taken:
+    columns and weights are cast to int64 / float64 (copies, kept alive for the run),
+    output buffers must already be uint8 (resp. float64 / int32 landmark buffers) and
+    large enough, and device tensors must live on the context's device."""
 
     def __init__(self, ctx: Context | None = None):
         self.ctx = _context(ctx)
@@ -84,27 +90,61 @@ class BackboneStages:
             return a.data_ptr(), (GS_DEVICE if a.is_cuda else GS_HOST)
         return ptr(a), GS_HOST
 
-    def begin(self, edge_index, num_nodes: int, edge_weights, epsilon: float, part: int,
-              nparts: int) -> int:
-        """Graph, columns by row, landmark searches l = part (mod nparts); returns K."""
+    def _on_device(self, t: torch.Tensor, what: str) -> None:
+        if t.is_cuda and t.device.index != self.ctx.device:
+            raise ValueError(f"{what} is on {t.device}, the context drives cuda:{self.ctx.device}")
+
+    def _out(self, buf, dtype, count: int, what: str):
+        """An output buffer the library writes `count` elements of `dtype` into."""
+        if isinstance(buf, torch.Tensor):
+            tdt = {np.uint8: torch.uint8, np.float64: torch.float64, np.int32: torch.int32}[dtype]
+            if buf.dtype != tdt:
+                raise TypeError(f"{what} must be {tdt}, got {buf.dtype}")
+            if not buf.is_contiguous():
+                raise ValueError(f"{what} must be contiguous")
+            self._on_device(buf, what)
+            n = buf.numel()
+        else:
+            if not isinstance(buf, np.ndarray) or buf.dtype != dtype or not buf.flags.c_contiguous:
+                raise TypeError(f"{what} must be a contiguous {np.dtype(dtype)} array")
+            n = buf.size
+        if n < count:
+            raise ValueError(f"{what} holds {n} entries, the library writes {count}")
+        return self._p(buf)
+
+    def _columns(self, edge_index, edge_weights):
+        """(src, dst, w) as int64 / int64 / float64 on one side, E, and their pointers."""
         if isinstance(edge_index, torch.Tensor) and edge_index.is_cuda:
-            src, dst = edge_index[0].contiguous(), edge_index[1].contiguous()
+            self._on_device(edge_index, "edge_index")
+            if edge_index.dim() != 2 or edge_index.shape[0] != 2:
+                raise ValueError("edge_index must be [2, E]")
+            src = edge_index[0].to(torch.int64).contiguous()
+            dst = edge_index[1].to(torch.int64).contiguous()
             E = int(src.numel())
         else:
-            ei = np.asarray(edge_index, dtype=np.int64)
+            ei = np.asarray(edge_index.cpu() if isinstance(edge_index, torch.Tensor) else edge_index,
+                            dtype=np.int64)
             E = ei.shape[1]
             src, dst = np.ascontiguousarray(ei[0]), np.ascontiguousarray(ei[1])
         if isinstance(edge_weights, torch.Tensor) and edge_weights.is_cuda:
-            w = edge_weights.reshape(-1)[:E].contiguous()
+            self._on_device(edge_weights, "edge_weights")
+            w = edge_weights.reshape(-1)[:E].to(torch.float64).contiguous()
         else:
-            w = np.ascontiguousarray(np.asarray(edge_weights, dtype=np.float64).reshape(-1)[:E])
+            ew = edge_weights.cpu() if isinstance(edge_weights, torch.Tensor) else edge_weights
+            w = np.ascontiguousarray(np.asarray(ew, dtype=np.float64).reshape(-1)[:E])
         check_weights(w, E)
         (ps, loc), (pd, _), (pw, wloc) = self._p(src), self._p(dst), self._p(w)
         if loc != wloc:
             raise ValueError("edge_index and edge_weights must be on the same side")
         self._keep_alive = (src, dst, w)
+        return E, ps, pd, pw, len(w), loc
+
+    def begin(self, edge_index, num_nodes: int, edge_weights, epsilon: float, part: int,
+              nparts: int) -> int:
+        """Graph, columns by row, landmark searches l = part (mod nparts); returns K."""
+        E, ps, pd, pw, nw, loc = self._columns(edge_index, edge_weights)
         K = ctypes.c_int32(0)
-        self.ctx.call("gs_bb_begin", int(num_nodes), E, ps, pd, pw, len(w), loc, float(epsilon),
+        self.ctx.call("gs_bb_begin", int(num_nodes), E, ps, pd, pw, nw, loc, float(epsilon),
                       int(part), int(nparts), ctypes.byref(K))
         self.n, self.E, self.K = int(num_nodes), E, int(K.value)
         return self.K
@@ -113,36 +153,30 @@ class BackboneStages:
                   nparts: int, keep):
         """gs_metric_backbone_part: keep bytes of the columns (u, v) with max(u, v) %
         nparts == part (ids as the library labels them), 0 elsewhere, into `keep`."""
-        if isinstance(edge_index, torch.Tensor) and edge_index.is_cuda:
-            src, dst = edge_index[0].contiguous(), edge_index[1].contiguous()
-            E = int(src.numel())
-        else:
-            ei = np.asarray(edge_index, dtype=np.int64)
-            E = ei.shape[1]
-            src, dst = np.ascontiguousarray(ei[0]), np.ascontiguousarray(ei[1])
-        if isinstance(edge_weights, torch.Tensor) and edge_weights.is_cuda:
-            w = edge_weights.reshape(-1)[:E].contiguous()
-        else:
-            w = np.ascontiguousarray(np.asarray(edge_weights, dtype=np.float64).reshape(-1)[:E])
-        check_weights(w, E)
-        (ps, loc), (pd, _), (pw, wloc), (pk, kloc) = self._p(src), self._p(dst), self._p(w), self._p(keep)
-        if loc != wloc:
-            raise ValueError("edge_index and edge_weights must be on the same side")
+        E, ps, pd, pw, nw, loc = self._columns(edge_index, edge_weights)
+        pk, kloc = self._out(keep, np.uint8, max(E, 1), "keep")
         relax = ctypes.c_int64(0)
-        self.ctx.call("gs_metric_backbone_part", int(num_nodes), E, ps, pd, pw, len(w), loc,
+        self.ctx.call("gs_metric_backbone_part", int(num_nodes), E, ps, pd, pw, nw, loc,
                       float(epsilon), int(part), int(nparts), pk, kloc, ctypes.byref(relax))
         self.relax = relax.value
         return keep
 
     def landmarks_io(self, D, complete, out: bool):
-        (pD, loc), (pc, _) = self._p(D), self._p(complete)
+        if self.K == 0 or self.E == 0:
+            return  # the library copies nothing then
+        pD, loc = self._out(D, np.float64, self.K * self.n, "landmark labels D")
+        pc, cloc = self._out(complete, np.int32, self.K, "landmark completeness flags")
+        if loc != cloc:
+            raise ValueError("D and complete must be on the same side")
         self.ctx.call("gs_bb_landmarks_io", pD, pc, loc, 0 if out else 1)
 
     def certify(self, part: int, nparts: int):
         self.ctx.call("gs_bb_certify", int(part), int(nparts))
 
     def state_io(self, state, out: bool):
-        p, loc = self._p(state)
+        if self.E == 0:
+            return
+        p, loc = self._out(state, np.uint8, self.E, "state")
         self.ctx.call("gs_bb_state_io", p, loc, 0 if out else 1)
 
     def plan(self) -> int:
@@ -157,12 +191,41 @@ class BackboneStages:
         """Keep bytes of every column (into ``keep`` if given) and the relaxations."""
         if keep is None:
             keep = np.zeros(max(self.E, 1), dtype=np.uint8)
-        p, loc = self._p(keep)
+        p, loc = self._out(keep, np.uint8, max(self.E, 1), "keep")
         relax = ctypes.c_int64(0)
         self.ctx.call("gs_bb_finish", p, loc, ctypes.byref(relax))
         self._keep_alive = None
         self.relax = relax.value
         return keep, relax.value
+
+
+#: decision classes of gs_bb_class_counts (include/gsparse.h GS_BB_WHY_*)
+DECISION_CLASSES = ("open", "self_loop", "isolated", "degree1", "direct_edge", "local_bound",
+                    "landmark_components", "landmark_prune", "landmark_keep", "witness",
+                    "local_3_4_edge", "search_prune", "search_keep", "reverse_exact",
+                    "reverse_prune", "reverse_keep", "meet_in_middle")
+
+
+def record_decision_classes(on: bool = True, ctx: Context | None = None) -> None:
+    """Make the following backbone runs on ``ctx`` record which exact rule decided each
+    column (gs_bb_classes; a diagnostic for the parity tests)."""
+    _context(ctx).call("gs_bb_classes", 1 if on else 0)
+
+
+def decision_classes(ctx: Context | None = None, return_why: bool = False):
+    """Columns per decision class of the last backbone run on ``ctx`` (this rank's
+    decisions), as {class name: count}; with return_why also the per-column class bytes
+    (uint8[E], indices into DECISION_CLASSES)."""
+    c = _context(ctx)
+    counts = np.zeros(len(DECISION_CLASSES), dtype=np.int64)
+    E = ctypes.c_int64(0)
+    c.call("gs_bb_class_counts", ptr(counts), len(counts), None, 0, GS_HOST, ctypes.byref(E))
+    out = {name: int(v) for name, v in zip(DECISION_CLASSES, counts)}
+    if not return_why:
+        return out
+    why = np.zeros(max(E.value, 1), dtype=np.uint8)
+    c.call("gs_bb_class_counts", ptr(counts), len(counts), ptr(why), why.size, GS_HOST, None)
+    return out, why[: E.value]
 
 
 def compute_metric_backbone(

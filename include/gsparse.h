@@ -122,6 +122,38 @@ int gs_jaccard_shares(gs_ctx *ctx, int nparts, int64_t *row_cut, int64_t *owner_
 int gs_jaccard_part_counts(gs_ctx *ctx, int part, int nparts, uint32_t *counts, int loc);
 int gs_jaccard_from_counts(gs_ctx *ctx, int nparts, const uint32_t *counts, int64_t stride,
                            int c_loc, double *out, int loc);
+/* Distributed global top-k of Jaccard-T (GraphSparsifier.sparsify, core.py:229-240, over N
+ * ranks; SURVEY 8(e) "top-k alone: histogram all-reduce") without gathering scores.  Each
+ * rank selects over its own owner pairs (gs_jaccard_part_counts; a pair's two CSR entries
+ * share one score, multiplicity 2, a self-loop 1):
+ *   gs_jsel_begin   scores (scores may be NULL: this part's pairs, owner order) and keys of
+ *                   the own pairs; hist (device, GS_JSEL_BINS uint64) = the weighted
+ *                   histogram of the keys' top 12 bits.  0 < num_keep < nnz.
+ *   gs_jsel_step    hist holds the SUM over ranks of the last histogram: picks the digit
+ *                   of the cut's rank and writes the next digit's histogram into hist;
+ *                   GS_JSEL_PASSES calls (12 + 4 x 13 bits), *passes_left counts down.
+ *   gs_jsel_result  the cut score, the entries strictly beyond it and the tie block (the
+ *                   same on every rank, = gs_topk_mask's), and this rank's tied positions.
+ *   gs_jsel_tie_positions  this rank's tied CSR positions (npos >= my_tied).
+ *   gs_jsel_keep    keep bytes of the own pairs (bit 0 the owner entry, bit 1 the reverse
+ *                   entry).  need = num_keep - n_beyond; when 0 < need < n_tied the cut is
+ *                   ambiguous and tie_pos must hold every rank's tied positions (ntie =
+ *                   n_tied, any order): the block is resolved as np.argsort(kind='stable')
+ *                   resolves it (top: the highest positions; keep_lowest: the lowest).
+ *   gs_jsel_mask    every rank's keep bytes (part p's at keep_all + p * stride, an
+ *                   all-gather padded to stride) -> the CSR keep mask mask[nnz], bit-identical
+ *                   to gs_topk_mask on the gathered scores.
+ * Symmetric graphs with nnz < 2^31 (else GS_EUNSUPPORTED). */
+enum { GS_JSEL_BINS = 8192, GS_JSEL_PASSES = 5 };
+int gs_jsel_begin(gs_ctx *ctx, int part, int nparts, const uint32_t *counts, int c_loc,
+                  int64_t num_keep, int keep_lowest, uint64_t *hist, double *scores, int s_loc);
+int gs_jsel_step(gs_ctx *ctx, uint64_t *hist, int *passes_left);
+int gs_jsel_result(gs_ctx *ctx, double *cut, int64_t *n_beyond, int64_t *n_tied, int64_t *my_tied);
+int gs_jsel_tie_positions(gs_ctx *ctx, int64_t *pos, int64_t npos, int loc);
+int gs_jsel_keep(gs_ctx *ctx, const int64_t *tie_pos, int64_t ntie, int t_loc, int64_t need,
+                 uint8_t *keep, int k_loc);
+int gs_jsel_mask(gs_ctx *ctx, int nparts, const uint8_t *keep_all, int64_t stride, int k_loc,
+                 uint8_t *mask, int m_loc);
 /* calculate_adamic_adar_scores, metrics.py:67-121 (bit-exact).  c[w] =
  * 1/sqrt(max(log(deg_w+1),1e-10)) as NumPy computes it (metrics.py:104-108),
  * n values. */
@@ -246,6 +278,37 @@ int gs_bb_state_io(gs_ctx *ctx, uint8_t *state, int loc, int dir);
 int gs_bb_plan(gs_ctx *ctx, int64_t *nbatch);
 int gs_bb_search(gs_ctx *ctx, int64_t b0, int64_t b1, int part, int nparts);
 int gs_bb_finish(gs_ctx *ctx, uint8_t *keep, int keep_loc, int64_t *n_relax);
+
+/* Decision classes of the metric backbone (a diagnostic: which exact rule decided each
+ * column of metric_backbone.py:97-111's comparison).  gs_bb_classes(ctx, 1) makes the
+ * following backbone runs on ctx record a class byte per column; gs_bb_class_counts
+ * returns, for the last run, counts[k] = columns decided by class k on this rank
+ * (ncounts >= GS_BB_WHY_CLASSES; counts[GS_BB_WHY_OPEN] = columns this rank left to
+ * others) and, when why != NULL, the E class bytes (nwhy >= E, else GS_EINDEX;
+ * why_loc: GS_HOST / GS_DEVICE); n_columns (may be NULL) = E of that run. */
+enum {
+    GS_BB_WHY_OPEN = 0,
+    GS_BB_WHY_SELF,         /* self-loop: d(u, u) = 0 */
+    GS_BB_WHY_ISOLATED,     /* an endpoint without edges in G: keep */
+    GS_BB_WHY_DEG1,         /* an endpoint of degree 1 whose neighbour is the other: d = w_G */
+    GS_BB_WHY_DIRECT,       /* w > fl(w_G(u, v) + eps): prune */
+    GS_BB_WHY_LOCAL2,       /* local lower bound from both endpoints' least other edges: keep */
+    GS_BB_WHY_LM_COMP,      /* a complete landmark search reaches one endpoint only: keep */
+    GS_BB_WHY_LM_PRUNE,     /* landmark upper bound: prune */
+    GS_BB_WHY_LM_KEEP,      /* landmark lower bound: keep */
+    GS_BB_WHY_WITNESS,      /* 2-hop witness path: prune */
+    GS_BB_WHY_LOCAL34,      /* 2- / 3- / 4-edge local lower bound: keep */
+    GS_BB_WHY_SEARCH_PRUNE, /* the source row's bounded search: prune */
+    GS_BB_WHY_SEARCH_KEEP,  /* the source row's bounded search: keep */
+    GS_BB_WHY_REV_EXACT,    /* the reverse row's search, exact rule */
+    GS_BB_WHY_REV_PRUNE,    /* the reverse row's search, upper bound: prune */
+    GS_BB_WHY_REV_KEEP,     /* the reverse row's search, unreached within its bound: keep */
+    GS_BB_WHY_MITM,         /* meet-in-the-middle certificate (GSPARSE_BB_MITM=1) */
+    GS_BB_WHY_CLASSES
+};
+int gs_bb_classes(gs_ctx *ctx, int on);
+int gs_bb_class_counts(gs_ctx *ctx, int64_t *counts, int ncounts, uint8_t *why, int64_t nwhy,
+                       int why_loc, int64_t *n_columns);
 
 /* Exact shortest-path distances for nq node pairs (qs[q], qt[q]) (host arrays;
  * out host) in the graph metric_backbone.py:70-79 builds from the columns

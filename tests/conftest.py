@@ -32,7 +32,8 @@ def pytest_configure(config):
 
 def golden_names(include_big=True):
     names = sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "*.npz")))
-    names = [n for n in names if n != "karate_weighted" and not n.startswith("exact_er_")]
+    names = [n for n in names
+             if n != "karate_weighted" and not n.startswith("exact_er_") and not n.startswith("bb_")]
     if not include_big:
         names = [n for n in names if n != "roman_full"]
     return names

@@ -67,6 +67,107 @@ class OracleEngine:
         beyond = int((s < cut).sum()) if keep_lowest else int((s > cut).sum())
         return mask, float(cut), beyond, int((s == cut).sum())
 
+    # gs_jsel_*'s contract (include/gsparse.h), restated with NumPy: keys of this part's
+    # owner pairs, weighted radix histograms (12 + 4 x 13 bits), keep bytes, the mask
+    JSEL_BINS, JSEL_PASSES = 8192, 5
+
+    def _owners(self):
+        ip, ix = np.asarray(self.ip, dtype=np.int64), np.asarray(self.ix, dtype=np.int64)
+        rows = O.csr_rows(ip)
+        deg = np.diff(ip)
+        own = (deg[rows] > deg[ix]) | ((deg[rows] == deg[ix]) & (rows <= ix))
+        e = np.nonzero(own)[0]
+        rev = np.searchsorted(rows * self.n + ix, ix[e] * self.n + rows[e])
+        return e, rev, deg[rows[e]] + deg[ix[e]]
+
+    @staticmethod
+    def _key(v):
+        b = np.asarray(v, dtype=np.float64).view(np.uint64)
+        return np.where(b >> np.uint64(63), ~b, b | np.uint64(1 << 63))
+
+    def _hist(self, p):
+        shift, bits = (52, 12) if p == 0 else (52 - 13 * p, 13)
+        top = shift + bits
+        hmask = np.uint64(0) if top >= 64 else np.uint64(((1 << 64) - 1) ^ ((1 << top) - 1))
+        sel = (self._keys & hmask) == (np.uint64(self._prefix) & hmask)
+        d = (self._keys[sel] >> np.uint64(shift)) & np.uint64((1 << bits) - 1)
+        return np.bincount(d.astype(np.int64), weights=self._wt[sel], minlength=self.JSEL_BINS).astype(np.int64)
+
+    def jsel_begin(self, part, nparts, counts, num_keep, keep_lowest, hist, scores=None):
+        _, Oo = self.jaccard_shares(nparts)
+        a, b = int(Oo[part]), int(Oo[part + 1])
+        opos, orev, osum = (x[a:b] for x in self._owners())
+        cnt = np.asarray(counts[: b - a].numpy() if hasattr(counts, "numpy") else counts[: b - a],
+                         dtype=np.int64).astype(np.uint32).astype(np.float64)
+        uni = osum.astype(np.float64) - cnt
+        val = np.divide(cnt, uni, out=np.zeros_like(cnt), where=uni > 0)
+        self._keys, self._wt, self._pp = self._key(val), np.where(opos == orev, 1, 2), (opos, orev)
+        self._lowest, self._prefix, self._below, self._eq, self._pass = keep_lowest, 0, 0, 0, 0
+        self._rank = num_keep - 1 if keep_lowest else self.nnz - num_keep
+        hist.copy_(torch.from_numpy(self._hist(0)))
+        if scores is not None:
+            scores[: b - a] = torch.from_numpy(val)
+        return b - a
+
+    def jsel_step(self, hist):
+        p = self._pass
+        h = hist.numpy().astype(np.int64)[: 1 << (12 if p == 0 else 13)]
+        c = np.cumsum(h)
+        d = int(np.searchsorted(c, self._rank, side="right"))
+        acc = int(c[d - 1]) if d else 0
+        self._rank -= acc
+        self._below += acc
+        self._prefix |= d << (52 if p == 0 else 52 - 13 * p)
+        self._pass += 1
+        if self._pass == self.JSEL_PASSES:
+            self._eq = int(h[d])
+        else:
+            hist.copy_(torch.from_numpy(self._hist(self._pass)))
+        return self.JSEL_PASSES - self._pass
+
+    def jsel_result(self):
+        cut = int(self._prefix)
+        b = cut & ((1 << 63) - 1) if cut >> 63 else ~cut & ((1 << 64) - 1)
+        nb = self._below if self._lowest else self.nnz - self._below - self._eq
+        tied = self._keys == np.uint64(cut)
+        opos, orev = self._pp
+        self._tpos = np.concatenate([opos[tied], orev[tied & (orev != opos)]])
+        return float(np.array([b], dtype=np.uint64).view(np.float64)[0]), nb, self._eq, len(self._tpos)
+
+    def jsel_tie_positions(self, out):
+        out[: len(self._tpos)] = torch.from_numpy(self._tpos)
+        return out
+
+    def jsel_keep(self, tie_pos, ntie, need, out):
+        cut = np.uint64(self._prefix)
+        k = self._keys
+        opos, orev = self._pp
+        beyond = (k < cut) if self._lowest else (k > cut)
+        b = np.where(beyond, 3, 0).astype(np.uint8)
+        tied = k == cut
+        if need >= ntie:
+            b[tied] = 3
+        elif need > 0:
+            t = np.sort(tie_pos.numpy())
+            ra, rb = np.searchsorted(t, opos[tied]), np.searchsorted(t, orev[tied])
+            ka = ra < need if self._lowest else ra >= ntie - need
+            kb = rb < need if self._lowest else rb >= ntie - need
+            b[tied] = ka.astype(np.uint8) | (kb.astype(np.uint8) << 1)
+        out[: len(b)] = torch.from_numpy(b)
+        return out
+
+    def jsel_mask(self, nparts, keep_all, stride, out):
+        _, Oo = self.jaccard_shares(nparts)
+        opos, orev, _ = self._owners()
+        i = np.arange(len(opos))
+        r = np.searchsorted(Oo, i, side="right") - 1
+        kb = keep_all.numpy()[r * stride + (i - Oo[r])]
+        m = np.zeros(self.nnz, dtype=np.uint8)
+        m[orev] = (kb >> 1) & 1
+        m[opos] = np.where(orev == opos, kb & 1, kb & 1)
+        out[: self.nnz] = torch.from_numpy(m)
+        return out
+
     def er_prepare(self, k):
         self.k = k
         rows = O.csr_rows(self.ip)
@@ -189,6 +290,18 @@ def _worker(rank, world, port, name, q):
                 for tb in ("numpy", "stable"):
                     m, _ = sharded_sparsify(eng, comm, torch.from_numpy(jac), E, r, low, tie_break=tb)
                     masks[(r, low, tb)] = m.numpy().copy()
+        # Jaccard-T without the score exchange (gs_jsel_* protocol): the same kept sets
+        from gsparse.distributed import sharded_jaccard_topk
+
+        nnz = len(g["indices"])
+        jsel = {}
+        for r in (0.8, 0.5, 0.2):
+            for low in (False, True):
+                for tb in ("numpy", "stable"):
+                    m, info, sc = sharded_jaccard_topk(eng, comm, r, low, tie_break=tb)
+                    jsel[(r, low, tb)] = m[:nnz].numpy().astype(bool)
+                    if E == nnz:
+                        assert np.array_equal(jsel[(r, low, tb)], masks[(r, low, tb)]), (r, low, tb, info)
         bb = None
         if "backbone_jaccard" in g:
             from gsparse.distributed import sharded_backbone
@@ -199,12 +312,17 @@ def _worker(rank, world, port, name, q):
             bb1 = sharded_backbone(comm, g["edge_index"], int(g["num_nodes"]), g["cost_jaccard"],
                                    stages=OracleStages(S=1), phases=[i / 7 for i in range(1, 7)])
             assert np.array_equal(bb, bb1)
+            # ranks asking for different search ranges follow rank 0's (no
+            # mismatched collective counts)
+            bb2 = sharded_backbone(comm, g["edge_index"], int(g["num_nodes"]), g["cost_jaccard"],
+                                   stages=OracleStages(), phases=[0.3] if rank == 0 else [0.5, 0.7])
+            assert np.array_equal(bb, bb2)
         # every rank selected the same kept set
         allm = [None] * world
         dist.all_gather_object(allm, {k: v.tobytes() for k, v in masks.items()})
         assert all(a == allm[0] for a in allm)
         if rank == 0:
-            q.put((jac, jac_w, er, bb, masks))
+            q.put((jac, jac_w, er, bb, masks, jsel))
     finally:
         dist.destroy_process_group()
 
@@ -218,7 +336,7 @@ def test_sharded_equals_single(name, world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, name, q)) for r in range(world)]
     for p in procs:
         p.start()
-    jac, jac_w, er, bb, masks = q.get(timeout=600)
+    jac, jac_w, er, bb, masks, jsel = q.get(timeout=600)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -236,6 +354,11 @@ def test_sharded_equals_single(name, world):
             assert np.array_equal(m, g[f"mask_jaccard_{r}_{int(low)}"]), (r, low)
         if tb == "stable":
             assert np.array_equal(m, O.topk_mask(g["scores_jaccard"], E, r, low, kind="stable")), (r, low)
+    # the distributed select over CSR entries: np.argsort(kind='stable') of the scores
+    nnz = len(g["indices"])
+    for (r, low, tb), m in jsel.items():
+        if tb == "stable":
+            assert np.array_equal(m, O.topk_mask(g["scores_jaccard"], nnz, r, low, kind="stable")), (r, low)
 
 
 def test_tree_helpers():

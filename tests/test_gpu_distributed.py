@@ -372,3 +372,143 @@ def test_landmark_searches_spread_vs_one_workgroup(gs, nparts, monkeypatch):
             D1, C1 = got[("1", W, r)]
             assert np.array_equal(C1, C0), (W, r)
             assert bits_equal(D1, D0), (W, r)
+
+
+def _jsel_parts(ei, n, nparts, r, low, dev):
+    """gs_jsel_* with nparts parts, each on its own library context on the one GPU, the
+    all-reduces / all-gathers done here on the device: (mask, info, own-pair scores)."""
+    from gsparse._lib import Context
+    from gsparse.engine import Engine
+
+    engs = []
+    for _ in range(nparts):
+        ctx = Context(0)
+        ctx.set_graph_edge_index(n, np.ascontiguousarray(ei[0]), np.ascontiguousarray(ei[1]))
+        engs.append(Engine(ctx))
+    nnz = engs[0].nnz
+    _, Oo = engs[0].jaccard_shares(nparts)
+    sizes = np.diff(Oo)
+    stride = max(1, int(sizes.max()))
+    num_keep = int(nnz * r)
+    hists, scores = [], []
+    for p, e in enumerate(engs):
+        c = torch.zeros(stride, dtype=torch.int32, device=dev)
+        e.jaccard_part_counts(p, nparts, out=c)
+        h = torch.zeros(e.JSEL_BINS, dtype=torch.int64, device=dev)
+        s = torch.empty(max(1, int(sizes[p])), dtype=torch.float64, device=dev)
+        e.jsel_begin(p, nparts, c, num_keep, low, h, s)
+        hists.append(h)
+        scores.append(s[: int(sizes[p])])
+    left = engs[0].JSEL_PASSES
+    while left:
+        tot = torch.stack(hists).sum(0)
+        lefts = set()
+        for h, e in zip(hists, engs):
+            h.copy_(tot)
+            lefts.add(e.jsel_step(h))
+        assert len(lefts) == 1
+        left = lefts.pop()
+    res = [e.jsel_result() for e in engs]
+    assert len({x[:3] for x in res}) == 1  # every part agrees on the cut
+    cut, nb, nt, _ = res[0]
+    need = num_keep - nb
+    tie_all = None
+    if 0 < need < nt:
+        pos = []
+        for e, x in zip(engs, res):
+            t = torch.zeros(max(1, x[3]), dtype=torch.int64, device=dev)
+            e.jsel_tie_positions(t)
+            pos.append(t[: x[3]])
+        tie_all = torch.cat(pos)
+        assert tie_all.numel() == nt
+    kall = torch.zeros(nparts * stride, dtype=torch.uint8, device=dev)
+    for p, e in enumerate(engs):
+        e.jsel_keep(tie_all, nt, need, kall[p * stride:(p + 1) * stride])
+    masks = []
+    for e in engs:
+        m = torch.empty(nnz, dtype=torch.uint8, device=dev)
+        e.jsel_mask(nparts, kall, stride, m)
+        masks.append(m.cpu().numpy().astype(bool))
+    for m in masks[1:]:
+        assert np.array_equal(m, masks[0])
+    info = {"cut": cut, "beyond": nb, "tied": nt, "need": need}
+    return masks[0], info, [s.cpu().numpy() for s in scores]
+
+
+def _tie_graph():
+    """Many equal scores: a union of disjoint cliques and stars (Jaccard 1 inside a
+    clique, 0 / small values on the stars), plus a self-loop."""
+    rng = np.random.default_rng(11)
+    edges = []
+    base = 0
+    for _ in range(40):
+        k = int(rng.integers(3, 7))
+        nodes = np.arange(base, base + k)
+        for a in nodes:
+            for b in nodes:
+                if a != b:
+                    edges.append((a, b))
+        base += k
+    for _ in range(30):
+        k = int(rng.integers(2, 9))
+        for leaf in range(1, k + 1):
+            edges += [(base, base + leaf), (base + leaf, base)]
+        base += k + 1
+    edges.append((0, 0))
+    ei = np.asarray(edges, dtype=np.int64).T
+    return np.ascontiguousarray(ei), base
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 3, 8])
+def test_distributed_jaccard_select_vs_one_gpu(gs, nparts):
+    """gs_jsel_* (Jaccard-T without the score exchange, core.py:229-240): for every
+    retention ratio and both directions the parts' mask equals one GPU's gs_topk_mask on
+    the whole scores (= np.argsort(kind='stable')), the cut / beyond / tied counts match,
+    and every part's own-pair scores are the reference's Jaccard at its owner entries."""
+    from gsparse import graphs
+
+    dev = torch.device("cuda", 0)
+    cases = [("tie", *_tie_graph()), ("hub", *_hub_graph()), ("rmat14", graphs.rmat(14, 8, seed=5), 1 << 14)]
+    g = load_golden("roman2000")
+    cases.append(("roman2000", g["edge_index"], int(g["num_nodes"])))
+    for name, ei, n in cases:
+        ip, ix, _ = O.canonical_csr(ei, n)
+        ref = O.jaccard(ip, ix)
+        nnz = len(ref)
+        e1 = _engine(gs, ei, n)
+        rows = O.csr_rows(ip)
+        deg = np.diff(ip)
+        own = np.nonzero((deg[rows] > deg[ix]) | ((deg[rows] == deg[ix]) & (rows <= ix)))[0]
+        _, Oo = e1.jaccard_shares(nparts)
+        for r in (0.9, 0.5, 0.2, 0.05):
+            for low in (False, True):
+                m, info, sc = _jsel_parts(ei, n, nparts, r, low, dev)
+                single, cut, nb, nt = e1.topk_mask(ref, nnz, int(nnz * r), low)
+                assert np.array_equal(m, single), (name, r, low, info)
+                assert np.array_equal(m, O.topk_mask(ref, nnz, r, low, kind="stable")), (name, r, low)
+                assert (info["beyond"], info["tied"]) == (nb, nt) and info["cut"] == cut, (name, r, low)
+        for p in range(nparts):  # the own-pair scores (last case's parts) = the reference's
+            assert bits_equal(sc[p], ref[own[Oo[p]:Oo[p + 1]]]), (name, p)
+
+
+def test_nccl_jaccard_topk_world1(gs, nccl_world1):
+    """sharded_jaccard_topk through a real RCCL group (world 1, device tensors): the
+    mask equals one GPU's stable top-k; tie_break="numpy" equals the reference's
+    np.argsort rule on an ambiguous cut."""
+    from gsparse import graphs
+    from gsparse.distributed import Comm, sharded_jaccard_topk
+
+    comm = Comm(device=torch.device("cuda", 0))
+    ei, n = graphs.rmat(14, 8, seed=5), 1 << 14
+    e = _engine(gs, ei, n)
+    ip, ix, _ = O.canonical_csr(ei, n)
+    ref = O.jaccard(ip, ix)
+    nnz = len(ref)
+    for r in (0.8, 0.5, 0.2):
+        m, info, sc = sharded_jaccard_topk(e, comm, r, tie_break="stable")
+        assert m.is_cuda
+        assert np.array_equal(m[:nnz].cpu().numpy().astype(bool), O.topk_mask(ref, nnz, r, False, kind="stable")), r
+        mn, info_n, _ = sharded_jaccard_topk(e, comm, r, tie_break="numpy")
+        assert np.array_equal(mn[:nnz].cpu().numpy().astype(bool), O.topk_mask(ref, nnz, r, False)), r
+    m, info, _ = sharded_jaccard_topk(e, comm, 1.0)
+    assert bool(m[:nnz].all()) and info["beyond"] == nnz

@@ -241,3 +241,15 @@ def test_counter_join_skips_first_call_kernels():
     assert c["first_call_only"] == ["gs::k_jac_plan"]
     bb = b.kernel_counters(summ, "metric_backbone", 1.0)
     assert bb["FETCH_SIZE_KB"] == 5.0 and bb["first_call_only"] == []
+
+
+def test_citation_like_rejects_impossible_counts():
+    """more distinct citations than n (n - 1) / 2 pairs raise instead of
+    looping; the limit itself is reachable."""
+    from gsparse import graphs
+
+    with pytest.raises(ValueError):
+        graphs.citation_like(5, 11)
+    with pytest.raises(ValueError):
+        graphs.citation_like(1, 0)
+    assert graphs.citation_like(5, 10).shape == (2, 20)
