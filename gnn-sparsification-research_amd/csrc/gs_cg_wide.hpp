@@ -9,15 +9,29 @@
 #pragma once
 #include "gs_cg_reg.hpp"
 
-// -DGS_CG_QS=1: whole columns (x in registers) store q = L_reg p of the SpMV pass in the
-// column's own Xc output column (L2 / Infinity Cache scratch until x is written there at
+// GS_CG_QS (default 1): whole columns (x in registers) store q = L_reg p of the SpMV pass
+// in the column's own Xc output column (Infinity Cache scratch until x is written there at
 // the end), and the r update reads it back (GS_CG_QPRE slots ahead) instead of
-// recomputing the SpMV: one SpMV per iteration, the same arithmetic
+// recomputing the SpMV: one SpMV per iteration, the same arithmetic.  Roman, T = 8: r
+// update 15.8 -> 5.9 us per column-iteration, 210.7 -> 167.6 ms per step (-DGS_CG_QS=0:
+// the round-5 form; profiles/r06b/, r06c/, r06d/)
 #ifndef GS_CG_QS
-#define GS_CG_QS 0
+#define GS_CG_QS 1
 #endif
+// (Roman, T = 8: q read 8 slots ahead 167.6 ms per step, 4 ahead 173.7, 12 ahead 168.1;
+// profiles/r06d/)
 #ifndef GS_CG_QPRE
-#define GS_CG_QPRE 4
+#define GS_CG_QPRE 8
+#endif
+// cache policy bits of the q stores / loads: 2 = nt (streaming).  The 256 CUs' q columns
+// (46 MB) evict the ELL rows, diagonals and global p rows the SpMV gathers from the XCDs'
+// L2 with the default policy: 189.9 ms per step, 173.7 with nt (profiles/r06c/, r06d/)
+#ifndef GS_CG_QAUX
+#define GS_CG_QAUX 2
+#endif
+// cache policy bits of the split tail's x read-modify-write in Xc (q-in-registers form)
+#ifndef GS_CG_XAUX
+#define GS_CG_XAUX 0
 #endif
 
 namespace gs {
@@ -531,11 +545,12 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         const __amdgpu_buffer_rsrc_t xrs =
             __builtin_amdgcn_make_buffer_rsrc(A.Xc + ci * A.ldn, 0, (int)(A.n * 8), 0x00020000);
         auto xload = [&](int u) -> double {
-            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xrs, base * 8, 256 * G * u, 0));
+            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xrs, base * 8, 256 * G * u, GS_CG_XAUX));
         };
         auto xstore = [&](int u, double v) {
             __builtin_amdgcn_raw_buffer_store_b64(
-                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), xrs, base * 8, 256 * G * u, 0);
+                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), xrs, base * 8, 256 * G * u,
+                GS_CG_XAUX);
         };
         // QS: q of slot u to / from the Xc column (rows of slots past the lane's chain rows
         // are not this lane's: their offset lies past the buffer, so the store is dropped
@@ -543,11 +558,11 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         auto qstore = [&](int u, double v) {
             __builtin_amdgcn_raw_buffer_store_b64(
                 __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), xrs,
-                valid(u) ? base * 8 : kOob, 256 * G * u, 0);
+                valid(u) ? base * 8 : kOob, 256 * G * u, GS_CG_QAUX);
         };
         auto qload = [&](int u) -> double {
             return __builtin_bit_cast(
-                double, __builtin_amdgcn_raw_buffer_load_b64(xrs, valid(u) ? base * 8 : kOob, 256 * G * u, 0));
+                double, __builtin_amdgcn_raw_buffer_load_b64(xrs, valid(u) ? base * 8 : kOob, 256 * G * u, GS_CG_QAUX));
         };
         // r = b.copy(); rho_0 = b.b
         {

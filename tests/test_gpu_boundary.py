@@ -126,3 +126,42 @@ def test_inputs_just_produced_by_torch(gs, side_stream):
             data.x = xd + a[0, 0].float() * 0
             assert bits_equal(sp_.compute_scores("feature_cosine"), g["scores_feature_cosine"])
             del a, xd, ei32, data, sp_
+
+
+def test_backbone_stages_device_inputs_checked(gs):
+    """BackboneStages with device tensors of other dtypes -- an int32
+    edge_index and float32 weights are cast (the library reads 8 B per column), giving
+    the int64 / float64 mask; an output buffer of the wrong dtype, size or device is
+    refused before the library writes into it."""
+    from gsparse._lib import Context
+    from gsparse.metric_backbone import BackboneStages, backbone_mask
+
+    g = load_golden("rmat10")
+    ei, n = g["edge_index"], int(g["num_nodes"])
+    w = g["cost_jaccard"] if "cost_jaccard" in g else np.linspace(0.1, 2.0, ei.shape[1])
+    ref = backbone_mask(ei, n, w)
+    dev = torch.device("cuda", 0)
+    E = ei.shape[1]
+    for ei_t, w_t in ((torch.from_numpy(ei).to(dev).to(torch.int32), torch.from_numpy(w).to(dev).float()),
+                      (torch.from_numpy(ei).to(dev), torch.from_numpy(w).to(dev))):
+        st = BackboneStages(Context(0))
+        w32 = w_t.double() if w_t.dtype == torch.float32 else w_t
+        exp = backbone_mask(ei, n, w32.cpu().numpy())  # float32 weights: the rounded values
+        st.begin(ei_t, n, w_t, 1e-9, 0, 1)
+        st.certify(0, 1)
+        nb = st.plan()
+        st.search(0, nb, 0, 1)
+        keep = torch.zeros(E, dtype=torch.uint8, device=dev)
+        st.finish(keep)
+        assert np.array_equal(keep.cpu().numpy().astype(bool), exp)
+    assert np.array_equal(exp, ref)
+    st = BackboneStages(Context(0))
+    st.begin(torch.from_numpy(ei).to(dev), n, torch.from_numpy(w).to(dev), 1e-9, 0, 1)
+    with pytest.raises(TypeError):
+        st.state_io(torch.zeros(E, dtype=torch.int32, device=dev), out=True)
+    with pytest.raises(ValueError):
+        st.state_io(torch.zeros(E - 1, dtype=torch.uint8, device=dev), out=True)
+    with pytest.raises(TypeError):
+        st.pair_part(ei, n, w, 1e-9, 0, 1, np.zeros(E, dtype=np.int64))
+    with pytest.raises(ValueError):
+        st.pair_part(ei, n, w, 1e-9, 0, 1, np.zeros(E - 1, dtype=np.uint8))

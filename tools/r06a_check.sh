@@ -3,7 +3,7 @@
 # select, and the existing backbone / distributed tests
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/r06a
+O=gpurun_out/${R06A_TAG:-r06a}
 mkdir -p "$O"
 T="timeout -k 10"
 PT="python -u -m pytest -x -v -s --timeout 300 --timeout-method thread"
