@@ -14,18 +14,18 @@
 // the end), and the r update reads it back (GS_CG_QPRE slots ahead) instead of
 // recomputing the SpMV: one SpMV per iteration, the same arithmetic.  Roman, T = 8: r
 // update 15.8 -> 5.9 us per column-iteration, 210.7 -> 167.6 ms per step (-DGS_CG_QS=0:
-// the round-5 form; profiles/r06b/, r06c/, r06d/)
+// the round-5 form; profiles/r06_cg_ab/)
 #ifndef GS_CG_QS
 #define GS_CG_QS 1
 #endif
 // (Roman, T = 8: q read 8 slots ahead 167.6 ms per step, 4 ahead 173.7, 12 ahead 168.1;
-// profiles/r06d/)
+// profiles/r06_cg_ab/)
 #ifndef GS_CG_QPRE
 #define GS_CG_QPRE 8
 #endif
 // cache policy bits of the q stores / loads: 2 = nt (streaming).  The 256 CUs' q columns
 // (46 MB) evict the ELL rows, diagonals and global p rows the SpMV gathers from the XCDs'
-// L2 with the default policy: 189.9 ms per step, 173.7 with nt (profiles/r06c/, r06d/)
+// L2 with the default policy: 189.9 ms per step, 173.7 with nt (profiles/r06_cg_ab/)
 #ifndef GS_CG_QAUX
 #define GS_CG_QAUX 2
 #endif

@@ -148,6 +148,10 @@ void sort_pairs_u64_i64(gs_ctx *c, uint64_t *keys, int64_t *vals, int64_t n, int
 
 using namespace gs;
 
+namespace gs {
+void jsel_forget(gs_ctx *c);  // gs_jsel.hip: drop the select state kept for this context
+}
+
 extern "C" {
 
 int gs_api_version(void) { return GS_API_VERSION; }
@@ -184,6 +188,7 @@ int gs_create(int device, gs_ctx **out) {
 
 void gs_destroy(gs_ctx *c) {
     if (!c) return;
+    gs::jsel_forget(c);
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (auto &p : c->pending) {

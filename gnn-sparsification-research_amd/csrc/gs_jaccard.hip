@@ -331,7 +331,22 @@ __global__ void __launch_bounds__(256) k_jac_light(const int64_t *__restrict__ i
     }
 }
 
-__device__ __forceinline__ uint32_t jac_hash(int32_t x) { return (uint32_t)x * 2654435761u; }
+// GS_JAC_FASTHASH (default 1): the tables' multiplicative hash with a 24-bit odd multiplier
+// (v_mul_u32_u24, full rate, instead of v_mul_lo_u32, quarter rate): (x * K) mod 2^b is
+// still a bijection of [0, 2^b) for the quotient tables, whose ids are < 2^24
+// (jac_qparams); the int32 tables compare whole ids, so any hash is exact there
+#ifndef GS_JAC_FASTHASH
+#define GS_JAC_FASTHASH 1
+#endif
+static constexpr uint32_t kJacMul24 = 0x9E3779u;  // odd
+__device__ __forceinline__ uint32_t jac_mul(uint32_t x) {
+#if GS_JAC_FASTHASH
+    return __umul24(x, kJacMul24);
+#else
+    return x * 2654435761u;
+#endif
+}
+__device__ __forceinline__ uint32_t jac_hash(int32_t x) { return jac_mul((uint32_t)x); }
 
 // Owned entries of a task, staged in LDS: (list base, length, entry offset).
 // Entries with d_v > kJacSmall fill the front and are taken one per wave;
@@ -585,7 +600,7 @@ __global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ i
 
 // Quotient tables (classes in GS_JAC_Q16, when the ids fit): 16-bit slots, so the
 // same LDS holds twice the slots -- half the load factor, and the 32K-slot class
-// runs two workgroups per CU instead of one.  h = (x * kJacMul) mod 2^b is a
+// runs two workgroups per CU instead of one.  h = (x * K) mod 2^b (jac_mul) is a
 // bijection of [0, 2^b) (odd multiplier, n <= 2^b); its top bits pick the home
 // bucket, the low qb bits (the remainder) go into the slot with the bucket's
 // distance from home: slot = (d + 1) << qb | rem, 0 = empty.  (bucket, slot)
@@ -602,11 +617,29 @@ __global__ void __launch_bounds__(1024) k_jac_hash(const int64_t *__restrict__ i
 #ifndef GS_JAC_LOADS_Q8  // ... with this many list loads per lane in flight
 #define GS_JAC_LOADS_Q8 8
 #endif
-static constexpr uint32_t kJacMul = 2654435761u;
 
 // any zero 16-bit half in v
 __device__ __forceinline__ uint32_t jac_hz16(uint32_t v) {
     return (v - 0x00010001u) & ~v & 0x80008000u;
+}
+
+// any of the 8 16-bit slots of a bucket equal to t (t2 = t in both halves).  GS_JAC_PKMIN
+// (default 1): the packed 16-bit minimum of the four XORed words (v_pk_min_u16) has a zero
+// half iff some slot matches -- 4 XOR + 3 packed minima + one zero-half test instead of
+// four zero-half tests and their ORs
+#ifndef GS_JAC_PKMIN
+#define GS_JAC_PKMIN 1
+#endif
+__device__ __forceinline__ bool jac_bucket_has(const uint4 &q, uint32_t t2) {
+#if GS_JAC_PKMIN
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 a = __builtin_bit_cast(u16x2, q.x ^ t2), b = __builtin_bit_cast(u16x2, q.y ^ t2);
+    const u16x2 c = __builtin_bit_cast(u16x2, q.z ^ t2), d = __builtin_bit_cast(u16x2, q.w ^ t2);
+    const u16x2 m = __builtin_elementwise_min(__builtin_elementwise_min(a, b), __builtin_elementwise_min(c, d));
+    return jac_hz16(__builtin_bit_cast(uint32_t, m)) != 0;
+#else
+    return (jac_hz16(q.x ^ t2) | jac_hz16(q.y ^ t2) | jac_hz16(q.z ^ t2) | jac_hz16(q.w ^ t2)) != 0;
+#endif
 }
 
 struct JacQParams {
@@ -622,24 +655,21 @@ struct JacQProbe {
         uint32_t h;
     };
     __device__ __forceinline__ S first(int32_t x) const {
-        const uint32_t h = ((uint32_t)x * kJacMul) & p.hmask;
+        const uint32_t h = jac_mul((uint32_t)x) & p.hmask;
         return S{tab[h >> p.qb], h};
     }
     __device__ __forceinline__ bool done(int32_t, S s) const {
         const uint32_t home = s.h >> p.qb, rem = s.h & p.rmask;
         for (uint32_t d = 0;;) {
             const uint32_t t = ((d + 1) << p.qb) | rem, t2 = t | (t << 16);
-            if (jac_hz16(s.q.x ^ t2) | jac_hz16(s.q.y ^ t2) | jac_hz16(s.q.z ^ t2) |
-                jac_hz16(s.q.w ^ t2))
-                return true;
+            if (jac_bucket_has(s.q, t2)) return true;
             if ((s.q.w >> 16) == 0 || ++d > p.dmax) return false;
             s.q = tab[(home + d) & nbm];
         }
     }
     __device__ __forceinline__ bool check1(int32_t, S s, bool &more) const {
         const uint32_t t = (1u << p.qb) | (s.h & p.rmask), t2 = t | (t << 16);
-        const bool hit = (jac_hz16(s.q.x ^ t2) | jac_hz16(s.q.y ^ t2) | jac_hz16(s.q.z ^ t2) |
-                          jac_hz16(s.q.w ^ t2)) != 0;
+        const bool hit = jac_bucket_has(s.q, t2);
         more = !hit && (s.q.w >> 16) != 0 && p.dmax >= 1;
         return hit;
     }
@@ -688,7 +718,7 @@ __global__ void __launch_bounds__(NT, MINW) k_jac_hashq(const int64_t *__restric
     jac_stage(ip, ix, u, du, lo, hi, st);
     uint32_t *words = reinterpret_cast<uint32_t *>(tab);
     for (int64_t e = a + threadIdx.x; e < a + du; e += blockDim.x) {
-        const uint32_t h = ((uint32_t)ix[e] * kJacMul) & qp.hmask;
+        const uint32_t h = jac_mul((uint32_t)ix[e]) & qp.hmask;
         const uint32_t home = h >> qp.qb, rem = h & qp.rmask;
         bool in = false;
         for (uint32_t d = 0; d <= qp.dmax && !in; ++d) {

@@ -215,6 +215,11 @@ __global__ void k_jsel_mask(const uint32_t *__restrict__ slot, const uint8_t *__
     }
 }
 
+void jsel_forget(gs_ctx *c) {
+    std::lock_guard<std::mutex> lk(g_jsel_mu);
+    g_jsel.erase(c);
+}
+
 }  // namespace gs
 
 using namespace gs;
@@ -304,6 +309,7 @@ extern "C" int gs_jsel_step(gs_ctx *c, uint64_t *hist, int *passes_left) {
         GS_HIP(hipGetLastError());
         prof_end(c, t0, "jsel_pass", 9.0 * (double)H.npairs);
         if (passes_left) *passes_left = kJselPasses - H.pass;
+        sync_if_needed(c);  // hist (a device output) is complete on return
     });
 }
 
