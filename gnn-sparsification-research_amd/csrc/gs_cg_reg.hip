@@ -3,6 +3,10 @@
 // and its design notes are in gs_cg_reg.hpp.
 #include "gs_cg_reg.hpp"
 
+#ifndef GS_CG_XG
+#define GS_CG_XG 0
+#endif
+
 namespace gs {
 
 // ELL-8 copy of L_reg: overflow entry counts (rows longer than 8)
@@ -293,7 +297,9 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
         }
     }
     const int64_t wslots = P ? std::min<int64_t>(ncu, std::max<int64_t>(W, 1)) : slots;
-    double *pg = (double *)c->buf("er_reg_pg").ensure(sizeof(double) * (size_t)std::max<int64_t>(std::max<int64_t>(wslots, slots), 1) * ldn);
+    // (-DGS_CG_XG: the second half holds each whole-column workgroup's q scratch)
+    double *pg = (double *)c->buf("er_reg_pg").ensure(sizeof(double) * (GS_CG_XG ? 2 : 1) *
+                                                      (size_t)std::max<int64_t>(std::max<int64_t>(wslots, slots), 1) * ldn);
     A.ld = ld;
     A.ldn = ldn;
     A.col0 = col0;

@@ -33,6 +33,12 @@
 #ifndef GS_CG_XAUX
 #define GS_CG_XAUX 0
 #endif
+// -DGS_CG_XG=1 (A/B): whole columns keep x in their Xc column instead of registers (88
+// VGPRs freed at 44 slots), q in a per-workgroup scratch (the second half of A.pg); the r
+// update reads q, x and the global p rows GS_CG_QPRE slots ahead and writes x
+#ifndef GS_CG_XG
+#define GS_CG_XG 0
+#endif
 
 namespace gs {
 
@@ -97,6 +103,8 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     constexpr bool DBANK = V2 && G == 2;
     // q of the SpMV pass kept for the r update in the column's Xc column (GS_CG_QS)
     constexpr bool QS = GS_CG_QS && !QR && !SPLIT;
+    // (GS_CG_XG) whole columns in the x-in-Xc form with q stored, not kept in registers
+    constexpr bool QSX = GS_CG_XG && QR && !SPLIT;
     extern __shared__ double lds[];
     const int part = SPLIT ? (int)(blockIdx.x % (unsigned)A.P) : 0;
     const int group = SPLIT ? (int)(blockIdx.x / (unsigned)A.P) : (int)blockIdx.x;
@@ -540,7 +548,7 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
     const int64_t ncols = (A.gate && *A.gate == 0) ? 0 : A.ncols;
     for (int64_t ci = group; ci < ncols; ci += ngroups) {
         const int64_t c = A.col0 + ci;
-        double r[R], x[QR ? 1 : R], qr[QR ? R : 1];
+        double r[R], x[QR ? 1 : R], qr[QR && !QSX ? R : 1];
         // QR: x of the slots in this column's Xc rows (raw buffer; rows past n dropped)
         const __amdgpu_buffer_rsrc_t xrs =
             __builtin_amdgcn_make_buffer_rsrc(A.Xc + ci * A.ldn, 0, (int)(A.n * 8), 0x00020000);
@@ -563,6 +571,27 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
         auto qload = [&](int u) -> double {
             return __builtin_bit_cast(
                 double, __builtin_amdgcn_raw_buffer_load_b64(xrs, valid(u) ? base * 8 : kOob, 256 * G * u, GS_CG_QAUX));
+        };
+        // QSX: q scratch of this workgroup (the second half of A.pg, after every slot's p rows)
+        const __amdgpu_buffer_rsrc_t qsr = __builtin_amdgcn_make_buffer_rsrc(
+            A.pg + ((int64_t)gridDim.x + group) * A.ldn, 0, QSX ? (int)(A.n * 8) : 0, 0x00020000);
+        auto q2store = [&](int u, double v) {
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), qsr,
+                valid(u) ? base * 8 : kOob, 256 * G * u, GS_CG_QAUX);
+        };
+        auto q2load = [&](int u) -> double {
+            return __builtin_bit_cast(
+                double, __builtin_amdgcn_raw_buffer_load_b64(qsr, valid(u) ? base * 8 : kOob, 256 * G * u, GS_CG_QAUX));
+        };
+        auto xload2 = [&](int u) -> double {
+            return __builtin_bit_cast(
+                double, __builtin_amdgcn_raw_buffer_load_b64(xrs, valid(u) ? base * 8 : kOob, 256 * G * u, GS_CG_QAUX));
+        };
+        auto xstore2 = [&](int u, double v) {
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), xrs,
+                valid(u) ? base * 8 : kOob, 256 * G * u, GS_CG_QAUX);
         };
         // r = b.copy(); rho_0 = b.b
         {
@@ -756,7 +785,8 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
                     if constexpr (V2) {
                         if (valid(u)) qv = spmv2(rowof(u), eb[u], db[u], pv, u);
                     } else if (valid(u)) qv = spmv(rowof(u), eb[u], lb[u], pv, u);
-                    if constexpr (QR) qr[u] = qv;
+                    if constexpr (QSX) q2store(u, qv);
+                    else if constexpr (QR) qr[u] = qv;
                     if constexpr (QS) qstore(u, qv);
                     chain_step(acc, pv, qv, u);
                     __builtin_amdgcn_sched_barrier(0);
@@ -773,6 +803,52 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             const double pq = finish(acc_pq, side_p, side_q);
             const double alpha = rho_cur / pq;
             lap(2);
+            // QSX: x += alpha p, r -= alpha q with q, x and the global p rows read kPq slots
+            // ahead (the LDS p rows read in place), chains of r.r
+            if constexpr (QSX) {
+                launder();
+                double acc = 0.0;
+                constexpr int kPq = GS_CG_QPRE;
+                double qb[R], xb[R], pgb[R];
+                auto pre = [&](int u) {
+                    qb[u] = q2load(u);
+                    xb[u] = it > 0 ? xload2(u) : 0.0;
+                    // global p rows: their buffer load now (LDS rows read 0 here, in place below)
+                    const int cd = u < ulds ? 0 : code_of(rowof(u));
+                    pgb[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                            prs, cd >= 0x8000 && valid(u) ? (cd & 0x7fff) * 8 + poff : kOob,
+                                                            0, kAux));
+                };
+#pragma unroll
+                for (int u = 0; u < kPq && u < R; ++u) pre(u);
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    if (u + kPq < R) pre(u + kPq);
+                    if (valid(u)) {
+                        double pu;
+                        if (u < ulds) {
+                            pu = lds_at(lds0() + 256u * G * u);
+                        } else {
+                            const int cd = code_of(rowof(u));
+                            const double lv = spl[cd < 0x8000 ? cd : zslot];
+                            pu = cd < 0x8000 ? lv : pgb[u];
+                        }
+                        const double t1 = alpha * pu;
+                        xstore2(u, xb[u] + t1);
+                        const double t2 = alpha * qb[u];
+                        r[u] = r[u] - t2;
+                    }
+                    chain_step(acc, r[u], r[u], u, true);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (g == 0 && live) acc_rr[chain] = acc;
+                if (tail) {
+                    const double t1 = alpha * side_p[tix];
+                    side_x[tix] = side_x[tix] + t1;
+                    const double t2 = alpha * side_q[tix];
+                    side_r[tix] = side_r[tix] - t2;
+                }
+            } else
             // QR: x += alpha p (x from / to Xc, p from LDS), r -= alpha q (q in registers),
             // chains of r.r
             if constexpr (QR) {
@@ -936,7 +1012,8 @@ __global__ void __launch_bounds__(kRegThreads) k_cg_regwide(RegArgs A) {
             }                                                                                 \
         };                                                                                    \
         (void)A.qreg; /* whole columns keep x in registers (the q-in-registers form of */     \
-        pick(std::false_type{}); /* round 2 lives on only in the split tail) */               \
+        /* round 2 lives on only in the split tail; GS_CG_XG: x in Xc, q stored) */           \
+        pick(std::integral_constant<bool, (bool)GS_CG_XG>{});                                 \
     }
 
 // one launch of the split form (q in registers), grid = groups x A.P workgroups
