@@ -2,7 +2,8 @@
 
 * ApproxER at configs[1] size in the bench's own configuration: the Roman-like
   graph, k = 2,674 JL columns, 500 CG iterations, the OpenBLAS ddot order of 8
-  threads (``--blas-threads`` default), the default CG mode (5: the
+  threads (``--blas-threads`` default) and of 16 (the box's default, the drop-in
+  API's order), the default CG mode (5: the
   register-resident solver).  The whole solve runs as the bench runs it, then
   the first round of whole columns (``k_cg_regwide<2,44>``, columns [0, 256))
   and the split tail (columns [2560, 2674), two workgroups per column) are read
@@ -35,10 +36,13 @@ def _host_threads() -> int:
     return max(1, min(16, n))
 
 
-@pytest.fixture(scope="module")
-def roman_t8():
+@pytest.fixture(scope="module", params=[8, 16])
+def roman_t8(request):
     """The bench's Roman step (bench.py main(): er_prepare -> device normal stream ->
-    er_solve(0, k, 500, 1e-6, 8)), with Z of the two pinned column blocks."""
+    er_solve(0, k, 500, 1e-6, T)), with Z of the two pinned column blocks: T = 8 (the
+    headline's OpenBLAS order) and T = 16 (the box's default thread count, the drop-in
+    API's order -- bench.py's box_blas_order line)."""
+    T = request.param
     from gsparse import graphs
     from gsparse._lib import Context
     from gsparse.engine import Engine, jl_dim
@@ -53,14 +57,14 @@ def roman_t8():
     ctx.profile_reset()
     eng.er_prepare(k)
     eng.er_project_device(np.random.default_rng(42), k)
-    eng.er_solve(0, k, 500, 1e-6, 8)
+    eng.er_solve(0, k, 500, 1e-6, T)
     prof = ctx.profile_read()
     ctx.profile(False)
     blocks = {"first_round": (0, 256), "split_tail": (2560, k)}
     z = {name: eng.er_z(a, b) for name, (a, b) in blocks.items()}
     its = eng.er_iterations()
     scores = eng.er_scores(0, k, True)
-    return ei, n, k, blocks, z, its, prof, scores
+    return ei, n, k, blocks, z, its, prof, scores, T
 
 
 @pytest.fixture(scope="module")
@@ -95,7 +99,7 @@ def _oracle_cg_columns(L, Y, cols, blas_threads=8):
 def test_roman_t8_solve_takes_the_timed_kernels(roman_t8):
     """The solve ran the register-resident launch (cg_reg) and the split tail did
     not fall back (no hand-off abort): the kernels pinned below are the bench's."""
-    *_, prof, _ = roman_t8
+    *_, prof, _, _ = roman_t8
     assert "cg_reg" in prof, prof
     assert "cg_split_abort" not in prof, prof
 
@@ -104,11 +108,11 @@ def test_roman_t8_solve_takes_the_timed_kernels(roman_t8):
 def test_roman_t8_columns_bit_exact_vs_oracle_cg(roman_t8, roman_oracle_y, block):
     """Z columns of the timed T = 8 solve == the oracle's CG, bit for bit
     (metrics.py:284-289; north_star float tolerance 1e-5 asserted beside it)."""
-    _, n, k, blocks, z, its, _, _ = roman_t8
+    _, n, k, blocks, z, its, _, _, T = roman_t8
     _, _, _, Y, L = roman_oracle_y
     a, b = blocks[block]
     cols = list(range(a, b))
-    Zo, ito = _oracle_cg_columns(L, Y, cols)
+    Zo, ito = _oracle_cg_columns(L, Y, cols, blas_threads=T)
     assert np.array_equal(its[a:b], ito)
     assert (ito == 500).all()  # chain-like graph: every column runs to maxiter
     got = z[block]
@@ -121,7 +125,7 @@ def test_roman_t8_columns_bit_exact_vs_oracle_cg(roman_t8, roman_oracle_y, block
 def test_roman_t8_scores_from_pinned_blocks(roman_t8, roman_oracle_y):
     """Sanity of the read-out path: scores of the timed solve are finite, positive
     and clamped as metrics.py:293-297 clamps."""
-    *_, scores = roman_t8
+    *_, scores, _ = roman_t8
     assert np.isfinite(scores).all() and (scores >= 1e-10).all()
 
 
