@@ -14,11 +14,12 @@
 //   result  the cut, the entries strictly beyond it and the tie block, as one GPU's
 //           radix select gives them (every rank holds the same reduced histograms)
 //   ties    (an ambiguous cut only) this rank's tied CSR positions -> all-gather
-//   keep    a keep byte per own pair: bit 0 the owner entry, bit 1 its reverse entry;
-//           the tie block resolved as np.argsort(kind='stable') resolves it (top: the
-//           highest positions; keep_lowest: the lowest)      -> all-gather
-//   mask    every rank's keep bytes -> the whole CSR keep mask (a gather through a
-//           per-entry slot table cached per graph and part count)
+//   keep    a 2-bit keep code per own pair (bit 0 the owner entry, bit 1 its reverse
+//           entry), four per byte; the tie block resolved as np.argsort(kind='stable')
+//           resolves it (top: the highest positions; keep_lowest: the lowest)
+//                                                              -> all-gather (E / 8 bytes)
+//   mask    every rank's codes -> the whole CSR keep mask (a gather through a per-entry
+//           code index cached per graph and part count)
 // The mask is bit-identical to gs_topk_mask on the gathered scores (the device tie rule).
 #include "gs_internal.hpp"
 
@@ -161,34 +162,44 @@ __device__ __forceinline__ int64_t jsel_tie_rank(const uint64_t *__restrict__ ta
     return lo;
 }
 
-// mode 0: ties none kept, 1: all kept, 2: by rank in the sorted block
+// mode 0: ties none kept, 1: all kept, 2: by rank in the sorted block.  Keep codes are
+// 2 bits per pair (bit 0 the owner entry, bit 1 the reverse), four pairs per byte: one
+// thread per byte, so no two threads share one
+__device__ __forceinline__ uint32_t jsel_code(uint64_t k, uint64_t cut, int keep_lowest, int mode,
+                                              const uint64_t *__restrict__ tall, int64_t ntie, int64_t need,
+                                              int32_t pa, int32_t pb) {
+    if (k != cut) return (keep_lowest ? k < cut : k > cut) ? 3u : 0u;
+    if (mode != 2) return mode ? 3u : 0u;
+    const int64_t ra = jsel_tie_rank(tall, ntie, (uint64_t)pa);
+    const int64_t rb = jsel_tie_rank(tall, ntie, (uint64_t)pb);
+    const bool ka = keep_lowest ? ra < need : ra >= ntie - need;
+    const bool kb = keep_lowest ? rb < need : rb >= ntie - need;
+    return (ka ? 1u : 0u) | (kb ? 2u : 0u);
+}
+
 __global__ void k_jsel_keep(const uint64_t *__restrict__ keys, const int32_t *__restrict__ opos,
                             const int32_t *__restrict__ orev, int64_t obase, int64_t np,
                             const JselDev *__restrict__ st, int keep_lowest, int mode,
                             const uint64_t *__restrict__ tall, int64_t ntie, int64_t need,
                             uint8_t *__restrict__ keep) {
     const uint64_t cut = st->prefix;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = keys[i];
-        uint8_t b;
-        if (k != cut) {
-            b = (keep_lowest ? k < cut : k > cut) ? 3 : 0;
-        } else if (mode != 2) {
-            b = mode ? 3 : 0;
-        } else {
-            const int64_t ra = jsel_tie_rank(tall, ntie, (uint64_t)opos[obase + i]);
-            const int64_t rb = jsel_tie_rank(tall, ntie, (uint64_t)orev[obase + i]);
-            const bool ka = keep_lowest ? ra < need : ra >= ntie - need;
-            const bool kb = keep_lowest ? rb < need : rb >= ntie - need;
-            b = (ka ? 1 : 0) | (kb ? 2 : 0);
+    const int64_t nb = (np + 3) >> 2;
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < nb;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t b = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int64_t i = 4 * q + t;
+            if (i < np)
+                b |= jsel_code(keys[i], cut, keep_lowest, mode, tall, ntie, need, opos[obase + i],
+                               orev[obase + i]) << (2 * t);
         }
-        keep[i] = b;
+        keep[q] = (uint8_t)b;
     }
 }
 
-// per CSR entry: the slot of its pair's keep byte in the gathered buffer (part r's bytes
-// at r * stride), bit 31 set for the pair's reverse entry
+// per CSR entry: the code index of its pair in the gathered buffer (part r's codes from
+// r * 4 * stride, stride in bytes), bit 31 set for the pair's reverse entry
 __global__ void k_jsel_slots(const int32_t *__restrict__ opos, const int32_t *__restrict__ orev,
                              const int64_t *__restrict__ O, int P, int64_t stride, int64_t nown,
                              uint32_t *__restrict__ slot) {
@@ -200,18 +211,19 @@ __global__ void k_jsel_slots(const int32_t *__restrict__ opos, const int32_t *__
             if (O[mid] <= i) lo = mid;
             else hi = mid - 1;
         }
-        const uint32_t s = (uint32_t)(lo * stride + (i - O[lo]));
+        const uint32_t s = (uint32_t)(4 * lo * stride + (i - O[lo]));
         slot[opos[i]] = s;
         if (orev[i] != opos[i]) slot[orev[i]] = s | 0x80000000u;
     }
 }
 
+// the gathered codes (~E / 8 bytes: 8 MB at R-MAT-22, mostly L2-resident) read by code index
 __global__ void k_jsel_mask(const uint32_t *__restrict__ slot, const uint8_t *__restrict__ kall,
                             int64_t nnz, uint8_t *__restrict__ mask) {
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz;
          e += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t s = slot[e];
-        mask[e] = (kall[s & 0x7fffffffu] >> (s >> 31)) & 1;
+        const uint32_t s = slot[e], c = s & 0x7fffffffu;
+        mask[e] = (kall[c >> 2] >> (2 * (c & 3) + (s >> 31))) & 1;
     }
 }
 
@@ -380,16 +392,16 @@ extern "C" int gs_jsel_keep(gs_ctx *c, const int64_t *tie_pos, int64_t ntie, int
             while (eb < 64 && ((uint64_t)H.nnz >> eb)) ++eb;
             sort_keys_u64(c, tall, ntie, eb);
         }
-        const int64_t np = H.npairs;
-        uint8_t *dk = (uint8_t *)out_device(c, c->outbuf, keep, np ? np : 1, k_loc);
+        const int64_t np = H.npairs, nb = (np + 3) / 4;
+        uint8_t *dk = (uint8_t *)out_device(c, c->outbuf, keep, nb ? nb : 1, k_loc);
         hipEvent_t t0 = prof_begin(c);
         if (np)
-            k_jsel_keep<<<grid_for(np, 256, 65536), 256, 0, s>>>(
+            k_jsel_keep<<<grid_for(nb, 256, 65536), 256, 0, s>>>(
                 c->buf("jsel_keys").as<uint64_t>(), c->buf("jac_opos").as<int32_t>(), c->buf("jac_orev").as<int32_t>(),
                 H.obase, np, (const JselDev *)c->buf("jsel_state").ptr, H.keep_lowest, mode, tall, ntie, need, dk);
         GS_HIP(hipGetLastError());
-        prof_end(c, t0, "jsel_keep", 9.0 * (double)np);
-        finish_out(c, keep, dk, np, k_loc);
+        prof_end(c, t0, "jsel_keep", 16.25 * (double)np);
+        finish_out(c, keep, dk, nb, k_loc);
         if (mode == 2 && t_loc != GS_DEVICE) GS_HIP(hipStreamSynchronize(s));
     });
 }
@@ -403,10 +415,10 @@ extern "C" int gs_jsel_mask(gs_ctx *c, int nparts, const uint8_t *keep_all, int6
         hipStream_t s = c->stream;
         const JacShares &sh = jaccard_shares(c, nparts);
         for (int r = 0; r < nparts; ++r)
-            GS_CHECK(sh.O(r + 1) - sh.O(r) <= stride, GS_EINDEX,
-                     "part %d holds %lld owner pairs, more than the stride %lld", r,
+            GS_CHECK((sh.O(r + 1) - sh.O(r) + 3) / 4 <= stride, GS_EINDEX,
+                     "part %d holds %lld owner pairs, more than the stride %lld bytes of codes hold", r,
                      (long long)(sh.O(r + 1) - sh.O(r)), (long long)stride);
-        GS_CHECK((int64_t)nparts * stride < ((int64_t)1 << 31), GS_EUNSUPPORTED, "keep buffer past 2^31 bytes");
+        GS_CHECK(4 * (int64_t)nparts * stride < ((int64_t)1 << 31), GS_EUNSUPPORTED, "keep codes past 2^31");
         const int64_t nnz = c->g.nnz, nown = sh.O(nparts);
         JselHost &H = jsel_host(c);
         auto *slot = (uint32_t *)c->buf("jsel_slot").ensure(sizeof(uint32_t) * (nnz ? nnz : 1));
@@ -426,7 +438,7 @@ extern "C" int gs_jsel_mask(gs_ctx *c, int nparts, const uint8_t *keep_all, int6
         hipEvent_t t0 = prof_begin(c);
         if (nnz) k_jsel_mask<<<grid_for(nnz, 256, 65536), 256, 0, s>>>(slot, dk, nnz, dm);
         GS_HIP(hipGetLastError());
-        prof_end(c, t0, "jsel_mask", 6.0 * (double)nnz);
+        prof_end(c, t0, "jsel_mask", 5.25 * (double)nnz);
         finish_out(c, mask, dm, nnz, m_loc);
     });
 }

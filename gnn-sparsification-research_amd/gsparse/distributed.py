@@ -255,7 +255,7 @@ def sharded_jaccard_topk(engine, comm: Comm, retention_ratio: float, keep_lowest
     (gs_jaccard_part_counts), scores and keys them, and the ranks select the cut together
     by radix select over all-reduced histograms (gs_jsel_*: five passes, one SUM
     all-reduce of <= 64 KB each); an ambiguous tie block exchanges only its positions;
-    each rank then sends one keep byte per own pair (an all-gather of ~E / 2 bytes in
+    each rank then sends a 2-bit keep code per own pair (an all-gather of ~E / 8 bytes in
     all) and every rank writes the whole CSR keep mask.
 
     The kept set equals a single GPU's ``sparsify`` on the same scores: the device tie
@@ -305,6 +305,24 @@ def sharded_jaccard_topk(engine, comm: Comm, retention_ratio: float, keep_lowest
             dist.all_reduce(c, op=dist.ReduceOp.SUM, group=comm.group)
             t.copy_(c)
 
+    # device compute: the library's calls run without host waits (async: each call orders
+    # the library's stream after torch's and torch's after the library's, so the RCCL
+    # all-reduces in between see the histograms); only gs_jsel_result reads to the host
+    ctx = getattr(engine, "ctx", None)
+    go_async = ctx is not None and dev.type == "cuda" and not getattr(ctx, "_async", False)
+    if go_async:
+        ctx.set_async(True)
+    try:
+        return _jsel_select(engine, comm, dev, counts, stride, nnz, num_keep, keep_lowest, tie_break,
+                            mask, scores_out, all_reduce)
+    finally:
+        if go_async:
+            ctx.set_async(False)
+
+
+def _jsel_select(engine, comm, dev, counts, stride, nnz, num_keep, keep_lowest, tie_break, mask,
+                 scores_out, all_reduce):
+    """sharded_jaccard_topk's select, after the counts (see there)."""
     hist = torch.zeros(engine.JSEL_BINS, dtype=torch.int64, device=dev)
     engine.jsel_begin(comm.rank, comm.world, counts, num_keep, keep_lowest, hist, scores_out)
     left = engine.JSEL_PASSES
@@ -331,10 +349,11 @@ def sharded_jaccard_topk(engine, comm: Comm, retention_ratio: float, keep_lowest
         tie_all = comm.all_gather_padded(pos[:my_tied], tsz).to(dev)
         if tie_all.numel() != nt:
             raise RuntimeError(f"tie block: {tie_all.numel()} positions gathered, {nt} expected")
-    keep = torch.zeros(stride, dtype=torch.uint8, device=dev)
+    stride4 = (stride + 3) // 4  # 2-bit codes, four pairs per byte
+    keep = torch.zeros(stride4, dtype=torch.uint8, device=dev)
     engine.jsel_keep(tie_all, nt, need, keep)
     kall = comm.all_gather_flat(keep).to(dev)
-    engine.jsel_mask(comm.world, kall, stride, mask)
+    engine.jsel_mask(comm.world, kall, stride4, mask)
     return mask, info, scores_out
 
 

@@ -177,6 +177,7 @@ class Engine:
             sloc = self._loc(scores)
         self.ctx.call("gs_jsel_begin", int(part), int(nparts), ptr(counts), self._loc(counts),
                       int(num_keep), int(bool(keep_lowest)), ptr(hist), ptr(scores), sloc)
+        self._jsel_pairs = np_
         return np_
 
     def jsel_step(self, hist) -> int:
@@ -202,10 +203,12 @@ class Engine:
         return out
 
     def jsel_keep(self, tie_pos, ntie: int, need: int, out):
-        """Keep bytes of this part's pairs (bit 0 owner entry, bit 1 reverse entry)."""
+        """2-bit keep codes of this part's pairs (bit 0 owner entry, bit 1 reverse entry),
+        four pairs per byte, into ``out`` (uint8, >= ceil(pairs / 4) bytes)."""
         import torch
 
-        self._need(out, 0, (np.uint8, torch.uint8), "keep")
+        np_ = getattr(self, "_jsel_pairs", 0)
+        self._need(out, (np_ + 3) // 4, (np.uint8, torch.uint8), "keep")
         tloc = GS_HOST
         if tie_pos is not None:
             self._need(tie_pos, ntie, (np.int64, torch.int64), "tie positions")
@@ -214,7 +217,7 @@ class Engine:
         return out
 
     def jsel_mask(self, nparts: int, keep_all, stride: int, out):
-        """Every part's keep bytes (part p at p * stride) -> the CSR keep mask (uint8)."""
+        """Every part's keep codes (part p's from byte p * stride) -> the CSR keep mask (uint8)."""
         import torch
 
         self._need(keep_all, nparts * stride, (np.uint8, torch.uint8), "keep_all")

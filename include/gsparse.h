@@ -135,12 +135,13 @@ int gs_jaccard_from_counts(gs_ctx *ctx, int nparts, const uint32_t *counts, int6
  *   gs_jsel_result  the cut score, the entries strictly beyond it and the tie block (the
  *                   same on every rank, = gs_topk_mask's), and this rank's tied positions.
  *   gs_jsel_tie_positions  this rank's tied CSR positions (npos >= my_tied).
- *   gs_jsel_keep    keep bytes of the own pairs (bit 0 the owner entry, bit 1 the reverse
- *                   entry).  need = num_keep - n_beyond; when 0 < need < n_tied the cut is
+ *   gs_jsel_keep    2-bit keep codes of the own pairs (bit 0 the owner entry, bit 1 the
+ *                   reverse entry), pair i in bits 2 (i % 4) of byte i / 4: ceil(pairs / 4)
+ *                   bytes.  need = num_keep - n_beyond; when 0 < need < n_tied the cut is
  *                   ambiguous and tie_pos must hold every rank's tied positions (ntie =
  *                   n_tied, any order): the block is resolved as np.argsort(kind='stable')
  *                   resolves it (top: the highest positions; keep_lowest: the lowest).
- *   gs_jsel_mask    every rank's keep bytes (part p's at keep_all + p * stride, an
+ *   gs_jsel_mask    every rank's codes (part p's at keep_all + p * stride bytes, an
  *                   all-gather padded to stride) -> the CSR keep mask mask[nnz], bit-identical
  *                   to gs_topk_mask on the gathered scores.
  * Symmetric graphs with nnz < 2^31 (else GS_EUNSUPPORTED). */

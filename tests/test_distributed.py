@@ -153,7 +153,11 @@ class OracleEngine:
             ka = ra < need if self._lowest else ra >= ntie - need
             kb = rb < need if self._lowest else rb >= ntie - need
             b[tied] = ka.astype(np.uint8) | (kb.astype(np.uint8) << 1)
-        out[: len(b)] = torch.from_numpy(b)
+        b4 = np.zeros((len(b) + 3) // 4 * 4, dtype=np.uint8)  # four 2-bit codes per byte
+        b4[: len(b)] = b
+        b4 = b4.reshape(-1, 4)
+        packed = (b4[:, 0] | (b4[:, 1] << 2) | (b4[:, 2] << 4) | (b4[:, 3] << 6)).astype(np.uint8)
+        out[: len(packed)] = torch.from_numpy(packed)
         return out
 
     def jsel_mask(self, nparts, keep_all, stride, out):
@@ -161,7 +165,8 @@ class OracleEngine:
         opos, orev, _ = self._owners()
         i = np.arange(len(opos))
         r = np.searchsorted(Oo, i, side="right") - 1
-        kb = keep_all.numpy()[r * stride + (i - Oo[r])]
+        c = 4 * r * stride + (i - Oo[r])
+        kb = (keep_all.numpy()[c >> 2] >> (2 * (c & 3))) & 3
         m = np.zeros(self.nnz, dtype=np.uint8)
         m[orev] = (kb >> 1) & 1
         m[opos] = np.where(orev == opos, kb & 1, kb & 1)

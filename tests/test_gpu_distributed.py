@@ -421,13 +421,14 @@ def _jsel_parts(ei, n, nparts, r, low, dev):
             pos.append(t[: x[3]])
         tie_all = torch.cat(pos)
         assert tie_all.numel() == nt
-    kall = torch.zeros(nparts * stride, dtype=torch.uint8, device=dev)
+    s4 = (stride + 3) // 4
+    kall = torch.zeros(nparts * s4, dtype=torch.uint8, device=dev)
     for p, e in enumerate(engs):
-        e.jsel_keep(tie_all, nt, need, kall[p * stride:(p + 1) * stride])
+        e.jsel_keep(tie_all, nt, need, kall[p * s4:(p + 1) * s4])
     masks = []
     for e in engs:
         m = torch.empty(nnz, dtype=torch.uint8, device=dev)
-        e.jsel_mask(nparts, kall, stride, m)
+        e.jsel_mask(nparts, kall, s4, m)
         masks.append(m.cpu().numpy().astype(bool))
     for m in masks[1:]:
         assert np.array_equal(m, masks[0])

@@ -59,7 +59,8 @@ for N in (1, 2, 4, 8):
     counts = [torch.zeros(stride, dtype=torch.int32, device=dev) for _ in range(N)]
     hists = [torch.zeros(e.JSEL_BINS, dtype=torch.int64, device=dev) for e in engs]
     scores = [torch.empty(max(1, int(s)), dtype=torch.float64, device=dev) for s in sizes]
-    kall = torch.zeros(N * stride, dtype=torch.uint8, device=dev)
+    s4 = (stride + 3) // 4
+    kall = torch.zeros(N * s4, dtype=torch.uint8, device=dev)
     masks = [torch.empty(nnz, dtype=torch.uint8, device=dev) for _ in range(N)]
     wall = np.zeros(N)
     dev_ms = np.zeros(N)
@@ -99,9 +100,9 @@ for N in (1, 2, 4, 8):
                 pos.append(t_[: x[3]])
             tie_all = torch.cat(pos)
         for r, e in enumerate(engs):
-            on(r, lambda: e.jsel_keep(tie_all, nt, need, kall[r * stride:(r + 1) * stride]))
+            on(r, lambda: e.jsel_keep(tie_all, nt, need, kall[r * s4:(r + 1) * s4]))
         for r, e in enumerate(engs):
-            on(r, lambda: e.jsel_mask(N, kall, stride, masks[r]))
+            on(r, lambda: e.jsel_mask(N, kall, s4, masks[r]))
         if rep == 0:
             same = all(bool(torch.equal(m, ref_mask)) for m in masks)
             rec["mask_equals_one_gpu_topk"] = same
@@ -122,7 +123,7 @@ for N in (1, 2, 4, 8):
                 "max_wall_ms": round(float(wall.max()) * 1e3 / reps, 3),
                 "max_device_ms": round(float(dev_ms.max()) / reps, 3),
                 "exchange_bytes": {"hist_allreduce_each": 8 * engs[0].JSEL_BINS, "passes": engs[0].JSEL_PASSES,
-                                   "keep_allgather_total": int(N * stride),
+                                   "keep_allgather_total": int(N * s4),
                                    "ties_allgather_total": int(8 * nt) if tie_all is not None else 0}})
     out["per_n"][N] = rec
     del ctxs, engs, counts, masks
