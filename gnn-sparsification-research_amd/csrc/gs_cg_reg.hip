@@ -240,7 +240,8 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
     // Split plan: the last round of columns, when it leaves at least half the CUs idle,
     // runs as groups of P workgroups per column (k_cg_regwide<..., SPLIT>), each part a
     // contiguous range of the BLAS chunks with all its rows' p in LDS.
-    // GSPARSE_REG_SPLIT=0: never; =P (>= 2): every column in P parts (tests).
+    // GSPARSE_REG_SPLIT=0: never; =P (>= 2): every column in P parts (tests);
+    // GSPARSE_REG_SPLIT_AUTO=1: the round-5 rule, two parts per tail column when they fit.
     int ncu = 256;
     GS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
     int P = 0;
@@ -253,11 +254,14 @@ void cg_regres_solve(gs_ctx *c, int64_t n, const int64_t *lp, const int32_t *li,
         if (forced >= 2) {
             P = std::min(forced, T);
             W = 0;
-        } else if (forced < 0 && !getenv("GSPARSE_CG_SLOTS")) {
-            // two parts per tail column whenever they fit: more parts only add hand-offs
-            // (Roman, 500 iterations: 78 tail columns in 2 / 3 / 4 parts 13.9 / 14.5 /
-            // 30.2 ms, 57 columns 13.7 / 14.3 / 15.5 ms, whole 21.8 ms;
-            // profiles/r03d/split_probe.txt)
+        } else if (forced < 0 && !getenv("GSPARSE_CG_SLOTS") && getenv("GSPARSE_REG_SPLIT_AUTO")) {
+            // (round 6: off by default.  With one SpMV per iteration a whole column-iteration
+            // takes ~31 us, and the last round solved whole inside the same launch -- each CU
+            // starts its tail column as soon as its own columns are done -- matches or beats
+            // the two-part split launch at every rank share: Roman 334 / 669 / 1,337 / 2,674
+            // columns 28.6 / 44.0 / 88.1 / 164.2 ms whole vs 29.8 / 44.0 / 90.6 / 164.9 ms
+            // split; profiles/r06_cg_ab/rankcols_*.  Round 3, at 44 us: 78 tail columns in 2
+            // / 3 / 4 parts 13.9 / 14.5 / 30.2 ms, whole 21.8 ms.)
             const int64_t rounds = (ncols + ncu - 1) / ncu;
             const int64_t tailc = ncols - (rounds - 1) * ncu;
             if (2 * tailc <= ncu) {

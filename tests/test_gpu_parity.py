@@ -188,8 +188,9 @@ def test_er_column_blocks_in_every_mode(gs, chunked_er, mode, monkeypatch):
 
 def test_split_tail_in_offset_column_blocks(gs, chunked_er, monkeypatch):
     """Column blocks that start past column 0 and leave a split last round (each
-    block ~325 columns: one whole round of 256, then ~69 columns in 3 parts) give
-    the same bits as the whole solve with the split form disabled."""
+    block ~325 columns: one whole round of 256, then ~69 columns in parts; the automatic
+    split, GSPARSE_REG_SPLIT_AUTO=1) give the same bits as the whole solve with the split
+    form disabled."""
     monkeypatch.setenv("GSPARSE_CG_MODE", "5")
     n, graphs_ = chunked_er
     ei, _ = graphs_["unit"]
@@ -202,6 +203,7 @@ def test_split_tail_in_offset_column_blocks(gs, chunked_er, monkeypatch):
     e.er_solve(0, k, 40, 1e-6, 8)
     whole = e.er_scores(0, k, finalize=False).copy()
     monkeypatch.delenv("GSPARSE_REG_SPLIT")
+    monkeypatch.setenv("GSPARSE_REG_SPLIT_AUTO", "1")  # the automatic split (off by default)
     b = gs.engine.er_split(k, 2)
     assert 256 < int(b[1]) - int(b[0]) <= 384 and 256 < int(b[2]) - int(b[1]) <= 384
     sums = []

@@ -6,8 +6,9 @@
   API's order), the default CG mode (5: the
   register-resident solver).  The whole solve runs as the bench runs it, then
   the first round of whole columns (``k_cg_regwide<2,44>``, columns [0, 256))
-  and the split tail (columns [2560, 2674), two workgroups per column) are read
-  back and compared bit for bit with the oracle's CG (oracle.c: SciPy 1.15's
+  and the last, partly occupied round (columns [2560, 2674): whole columns inside the
+  same launch since round 6; the split form is pinned by the forced-split parity
+  tests) are read back and compared bit for bit with the oracle's CG (oracle.c: SciPy 1.15's
   recurrence, OpenBLAS-SkylakeX ddot for 8 threads) on the same Y columns.
   Reference: metrics.py:272-289.
 * The metric backbone (configs[4]) at the bench's sizes: the full Roman-like
