@@ -87,7 +87,7 @@ __global__ void k_bb_keys(const int64_t *__restrict__ src, const int64_t *__rest
         const int64_t os = osrc[i], od = odst[i];
         if (os < 0 || os >= n || od < 0 || od >= n) {
             atomicOr(bad, 1);
-            keys[i] = ~0ull;
+            keys[i] = (uint64_t)n * (uint64_t)n;
             idx[i] = i;
             continue;
         }
@@ -96,7 +96,7 @@ __global__ void k_bb_keys(const int64_t *__restrict__ src, const int64_t *__rest
         if (!(x >= 0.0)) atomicOr(bad, 2);  // negative or NaN weight
         // undirected edges from s<d columns (caller's ids); others sort to the end
         const uint64_t lo = (uint64_t)(s < d ? s : d), hi = (uint64_t)(s < d ? d : s);
-        keys[i] = os < od ? lo * (uint64_t)n + hi : ~0ull;
+        keys[i] = os < od ? lo * (uint64_t)n + hi : (uint64_t)n * (uint64_t)n;
         idx[i] = i;
     }
 }
@@ -109,7 +109,7 @@ __global__ void k_bb_unique(const uint64_t *__restrict__ keys, const int64_t *__
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
          i += (int64_t)gridDim.x * blockDim.x) {
         uint64_t k = keys[i];
-        if (k == ~0ull) continue;
+        if (k >= (uint64_t)n * (uint64_t)n) continue;
         if (i > 0 && keys[i - 1] == k) continue;
         double m = w[idx[i]];
         for (int64_t j = i + 1; j < E && keys[j] == k; ++j) {
@@ -133,24 +133,40 @@ __global__ void k_bb_sym_payload(int64_t cnt2, int64_t *__restrict__ pay) {
 
 __global__ void k_bb_gfill(const uint64_t *__restrict__ skeys, const int64_t *__restrict__ pay,
                            const double *__restrict__ uw, int64_t cnt2, int64_t n,
-                           int32_t *__restrict__ gi, double *__restrict__ gw,
-                           unsigned long long *__restrict__ deg) {
+                           int32_t *__restrict__ gi, double *__restrict__ gw) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cnt2;
          i += (int64_t)gridDim.x * blockDim.x) {
-        uint64_t k = skeys[i];
-        gi[i] = (int32_t)(k % (uint64_t)n);
+        gi[i] = (int32_t)(skeys[i] % (uint64_t)n);
         gw[i] = uw[pay[i]];
-        atomicAdd(&deg[k / (uint64_t)n], 1ull);
+    }
+}
+
+// row pointers of keys sorted by row = key / div (rows < n): ptr[r] = the first entry whose
+// key is >= r * div, one binary search per row (no atomics: an R-MAT hub's degree counted
+// by atomics on one address serialises -- the G fill and the columns-by-row pass took
+// 1.6 + 1.2 ms of RMAT-18's begin, round 5; and no per-entry loop over the empty rows
+// between entries: the degree relabeling puts ~40 % of the rows, all empty, last)
+__global__ void k_bb_rowptr(const uint64_t *__restrict__ keys, int64_t cnt, uint64_t div, int64_t n,
+                            int64_t *__restrict__ ptr) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r <= n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = (uint64_t)r * div;
+        int64_t lo = 0, hi = cnt;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (keys[mid] < t) lo = mid + 1;
+            else hi = mid;
+        }
+        ptr[r] = lo;
     }
 }
 
 __global__ void k_bb_srckeys(const int64_t *__restrict__ src, int64_t E, uint64_t *__restrict__ keys,
-                             int64_t *__restrict__ idx, unsigned long long *__restrict__ cnt) {
+                             int64_t *__restrict__ idx) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
          i += (int64_t)gridDim.x * blockDim.x) {
         keys[i] = (uint64_t)src[i];
         idx[i] = i;
-        atomicAdd(&cnt[src[i]], 1ull);
     }
 }
 
@@ -1840,6 +1856,23 @@ __global__ void k_bb_relabel_keys(const unsigned long long *__restrict__ cnt, in
     }
 }
 
+// landmark order: ascending ((2^32 - 1 - degree in G) << 32 | id) = by degree, high first,
+// ties by id (round 5's host partial_sort over a copy of G's row pointers)
+__global__ void k_bb_degkeys(const int64_t *__restrict__ gp, int64_t n, uint64_t *__restrict__ keys,
+                             int64_t *__restrict__ ids) {
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t d = (uint64_t)(gp[x + 1] - gp[x]);
+        keys[x] = ((0xffffffffull - (d < 0xffffffffull ? d : 0xffffffffull)) << 32) | (uint64_t)x;
+        ids[x] = x;
+    }
+}
+
+__global__ void k_bb_first_ids(const int64_t *__restrict__ ids, int K, int32_t *__restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < K) out[i] = (int32_t)ids[i];
+}
+
 __global__ void k_bb_perm(const int64_t *__restrict__ ids, int64_t n, int64_t *__restrict__ perm) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -1863,7 +1896,7 @@ __global__ void k_bb_map(const int64_t *__restrict__ perm, const int64_t *__rest
 static void bb_build_graph(gs_ctx *c, int64_t n, int64_t E, const int64_t *dsrc, const int64_t *ddst,
                            const int64_t *osrc, const int64_t *odst, const double *dw,
                            unsigned long long *misc, int64_t *&gp, int32_t *&gi, double *&gw,
-                           double *wmed = nullptr) {
+                           double *wmed = nullptr, int64_t *gnnz = nullptr) {
     hipStream_t s = c->stream;
     int *bad = (int *)(misc + 4);
     uint64_t *keys = (uint64_t *)c->buf("bb_keys").ensure(8 * E);
@@ -1876,7 +1909,7 @@ static void bb_build_graph(gs_ctx *c, int64_t n, int64_t E, const int64_t *dsrc,
     GS_CHECK(!(hbad & 1), GS_EINVAL, "edge_index entry out of range [0, %lld)", (long long)n);
     GS_CHECK(!(hbad & 2), GS_EUNSUPPORTED,
              "edge weights must be non-negative and not NaN (Dijkstra contract)");
-    sort_pairs_u64_i64(c, keys, idx, E, 64);
+    sort_pairs_u64_i64(c, keys, idx, E, bits_for_bb((uint64_t)n * (uint64_t)n));
     uint64_t *ukeys = (uint64_t *)c->buf("bb_ukeys").ensure(16 * E);
     double *uw = (double *)c->buf("bb_uw").ensure(8 * E);
     k_bb_unique<<<grid_for(E, 256, 8192), 256, 0, s>>>(keys, idx, dw, E, n, misc, ukeys, uw);
@@ -1884,6 +1917,7 @@ static void bb_build_graph(gs_ctx *c, int64_t n, int64_t E, const int64_t *dsrc,
     GS_HIP(hipMemcpyAsync(&ucnt, misc, 8, hipMemcpyDeviceToHost, s));
     GS_HIP(hipStreamSynchronize(s));
     int64_t cnt2 = 2 * (int64_t)ucnt;
+    if (gnnz) *gnnz = cnt2;
     if (wmed) {  // median of <= 1023 evenly spaced unique-edge weights
         *wmed = 0.0;
         if (ucnt) {
@@ -1902,12 +1936,8 @@ static void bb_build_graph(gs_ctx *c, int64_t n, int64_t E, const int64_t *dsrc,
     gp = (int64_t *)c->buf("bb_gp").ensure(8 * (n + 1));
     gi = (int32_t *)c->buf("bb_gi").ensure(4 * (cnt2 + 1));
     gw = (double *)c->buf("bb_gw").ensure(8 * (cnt2 + 1));
-    unsigned long long *deg = (unsigned long long *)c->buf("bb_flag").ensure(8 * (n + 1));
-    GS_HIP(hipMemsetAsync(deg, 0, 8 * (n + 1), s));
-    if (cnt2)
-        k_bb_gfill<<<grid_for(cnt2, 256, 8192), 256, 0, s>>>(ukeys, pay, uw, cnt2, n, gi, gw,
-                                                            deg);
-    exclusive_scan_i64(c, (const int64_t *)deg, gp, n + 1);
+    if (cnt2) k_bb_gfill<<<grid_for(cnt2, 256, 8192), 256, 0, s>>>(ukeys, pay, uw, cnt2, n, gi, gw);
+    k_bb_rowptr<<<grid_for(n + 1, 256, 8192), 256, 0, s>>>(ukeys, cnt2, (uint64_t)n, n, gp);
 }
 
 // ---------------------------------------------------------------------------
@@ -1950,7 +1980,6 @@ struct BbRun {
     int K = 0;
     double *D = nullptr;
     int32_t *lcomp = nullptr;
-    std::vector<int32_t> lm_ids;  // host source of an async copy: lives with the run
     int64_t nsrc = 0, nbatch = 0, slabs = 0;
     int S = 1, bt = 256;
     int64_t *sources = nullptr;
@@ -2073,16 +2102,15 @@ static void bb_begin(gs_ctx *c, int64_t n, int64_t E, const int64_t *src, const 
     R.tall = prof_begin(c);
     if (E > 0) {
         hipEvent_t t0 = prof_begin(c);  // ended as "bb_build" below (no leak at E = 0)
-        bb_build_graph(c, n, E, dsrc, ddst, osrc, odst, R.dw, R.misc, R.gp, R.gi, R.gw, &R.wmed);
-        unsigned long long *deg = (unsigned long long *)b_flag.ensure(8 * (n + 1));
+        int64_t gnnz = 0;
+        bb_build_graph(c, n, E, dsrc, ddst, osrc, odst, R.dw, R.misc, R.gp, R.gi, R.gw, &R.wmed, &gnnz);
         // columns grouped by source row (stable: radix sort is stable)
         uint64_t *okeys = (uint64_t *)b_okeys.ensure(8 * E);
         R.order = (int64_t *)b_order.ensure(8 * E);
         R.optr = (int64_t *)b_optr.ensure(8 * (n + 1));
-        GS_HIP(hipMemsetAsync(deg, 0, 8 * (n + 1), s));
-        k_bb_srckeys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, E, okeys, R.order, deg);
+        k_bb_srckeys<<<grid_for(E, 256, 8192), 256, 0, s>>>(dsrc, E, okeys, R.order);
         sort_pairs_u64_i64(c, okeys, R.order, E, bits_for_bb((uint64_t)n));
-        exclusive_scan_i64(c, (const int64_t *)deg, R.optr, n + 1);
+        k_bb_rowptr<<<grid_for(n + 1, 256, 8192), 256, 0, s>>>(okeys, E, 1, n, R.optr);
         prof_end(c, t0, "bb_build", 0.0);
         hipEvent_t tp = prof_begin(c);
         // landmark certificates (GSPARSE_BB_LANDMARKS = K, 0 = off; large graphs: 48 --
@@ -2093,19 +2121,13 @@ static void bb_begin(gs_ctx *c, int64_t n, int64_t E, const int64_t *src, const 
         if (K > n) K = (int)n;
         R.K = K;
         if (K > 0) {
-            // landmarks: the K highest-degree nodes of G
-            std::vector<int64_t> hgp(n + 1);
-            GS_HIP(hipMemcpyAsync(hgp.data(), R.gp, 8 * (n + 1), hipMemcpyDeviceToHost, s));
-            GS_HIP(hipStreamSynchronize(s));
-            R.lm_ids.resize(n);
-            for (int64_t x = 0; x < n; ++x) R.lm_ids[x] = (int32_t)x;
-            std::partial_sort(R.lm_ids.begin(), R.lm_ids.begin() + K, R.lm_ids.end(),
-                              [&](int32_t p, int32_t q) {
-                                  const int64_t dp = hgp[p + 1] - hgp[p], dq = hgp[q + 1] - hgp[q];
-                                  return dp != dq ? dp > dq : p < q;
-                              });
+            // landmarks: the K highest-degree nodes of G (ties: the lower id), on the device
+            uint64_t *dk = (uint64_t *)c->buf("bb_lmkeys").ensure(8 * n);
+            int64_t *di = (int64_t *)c->buf("bb_lmord").ensure(8 * n);
+            k_bb_degkeys<<<grid_for(n, 256, 8192), 256, 0, s>>>(R.gp, n, dk, di);
+            sort_pairs_u64_i64(c, dk, di, n, 64);
             int32_t *dlm = (int32_t *)b_lm.ensure(4 * K);
-            GS_HIP(hipMemcpyAsync(dlm, R.lm_ids.data(), 4 * K, hipMemcpyHostToDevice, s));
+            k_bb_first_ids<<<(unsigned)((K + 255) / 256), 256, 0, s>>>(di, K, dlm);
             R.D = (double *)b_land.ensure(8 * (size_t)K * n);
             k_bb_fill_u64<<<grid_for((int64_t)K * n, 256, 65536), 256, 0, s>>>(
                 (unsigned long long *)R.D, (int64_t)K * n, kInfBits);
@@ -2117,7 +2139,7 @@ static void bb_begin(gs_ctx *c, int64_t n, int64_t E, const int64_t *src, const 
             bool coop = n > 65536 && n < ((int64_t)1 << 31);
             if (const char *e = getenv("GSPARSE_BB_LMCOOP")) coop = coop && atoi(e) != 0;
             if (mine > 0 && coop) {
-                const int64_t cap = n + hgp[n] / kLmChunk + 64;  // items of one round, at most
+                const int64_t cap = n + gnnz / kLmChunk + 64;  // items of one round, at most
                 uint64_t *items = (uint64_t *)c->buf("bb_lmitems").ensure(16 * (size_t)mine * cap);
                 uint32_t *stamp = (uint32_t *)c->buf("bb_lmstamp").ensure(4 * (size_t)mine * n);
                 int32_t *cnt = (int32_t *)c->buf("bb_lmcnt").ensure(16 * (size_t)mine);
